@@ -1,0 +1,295 @@
+#!/usr/bin/env python3
+"""Throughput bench for the Word2Vec hot path on MI355X.
+
+Workload (BASELINE.json configs[2], the 1-GPU headline config): skip-gram,
+negative sampling neg=5, dim=300, window=5, subsample 1e-4, min_count 5, on a
+synthetic Zipf(s=1) corpus over 1M word ranks in 1000-token sentences (the
+1B-Word corpus is not available offline). One "step" = one training pass
+(epoch) of the hot path over this rank's shard, inputs already resident in HBM.
+With N GPUs (torchrun), every rank trains its own shard of the same size on a
+full model replica and the replicas are averaged with an RCCL all-reduce after
+every step (weak scaling).
+
+Prints ONE JSON line on rank 0 (metric/value/unit/... + roofline + cpu_baseline).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+MODES = {
+    "sg_ns": dict(cbow=False, hs=False),
+    "sg_hs": dict(cbow=False, hs=True),
+    "cbow_ns": dict(cbow=True, hs=False),
+    "cbow_hs": dict(cbow=True, hs=True),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--mode", default="sg_ns", choices=list(MODES))
+    ap.add_argument("--dim", type=int, default=300)
+    ap.add_argument("--negative", type=int, default=5)
+    ap.add_argument("--window", type=int, default=5)
+    ap.add_argument("--vocab", type=int, default=1_000_000, help="Zipf rank range (V before min_count)")
+    ap.add_argument("--tokens", type=int, default=50_000_000, help="raw tokens per GPU per step")
+    ap.add_argument("--sent-len", type=int, default=1000)
+    ap.add_argument("--subsample", type=float, default=1e-4)
+    ap.add_argument("--min-count", type=int, default=5)
+    ap.add_argument("--table-size", type=int, default=100_000_000)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
+    return ap.parse_args()
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from word2vec_amd import _native as N
+    from word2vec_amd import host
+    from word2vec_amd.device import Config, DeviceTrainer
+
+    mode = MODES[args.mode]
+    neg = 0 if mode["hs"] else args.negative
+    d = args.dim
+
+    # ---- synthetic corpus shard (on the GPU, seeded per rank) ------------------
+    t0 = time.time()
+    n_sent = args.tokens // args.sent_len
+    n_tok = n_sent * args.sent_len
+    g = torch.Generator(device=dev)
+    g.manual_seed(args.seed * 1000 + rank)
+    p = 1.0 / torch.arange(1, args.vocab + 1, device=dev, dtype=torch.float64)
+    cdf = torch.cumsum(p, 0)
+    cdf /= cdf[-1].clone()
+    ranks = torch.empty(n_tok, dtype=torch.int64, device=dev)
+    chunk = 1 << 24
+    for s in range(0, n_tok, chunk):
+        e = min(n_tok, s + chunk)
+        u = torch.rand(e - s, generator=g, device=dev, dtype=torch.float64)
+        ranks[s:e] = torch.searchsorted(cdf, u, right=True).clamp_(max=args.vocab - 1)
+        del u
+    counts = torch.bincount(ranks, minlength=args.vocab)
+    if world > 1:
+        dist.all_reduce(counts)  # one vocab for all replicas (built over the whole corpus)
+    order = torch.argsort(counts, descending=True, stable=True)
+    V = int((counts >= args.min_count).sum())
+    vocab_ranks = order[:V]
+    remap = torch.full((args.vocab,), -1, dtype=torch.int64, device=dev)
+    remap[vocab_ranks] = torch.arange(V, device=dev)
+    ids = remap[ranks]
+    del ranks
+    inv = ids >= 0
+    lens = inv.view(n_sent, args.sent_len).sum(1)
+    soff = torch.zeros(n_sent + 1, dtype=torch.int64, device=dev)
+    soff[1:] = torch.cumsum(lens, 0)
+    ids_iv = ids[inv].to(torch.int32)
+    del ids, inv
+    counts_v = counts[vocab_ranks].cpu().numpy().astype(np.int64)
+    ids_h = ids_iv.cpu().numpy()
+    soff_h = soff.cpu().numpy()
+    del ids_iv
+    log(f"[bench] corpus: {n_tok} raw tokens/rank, {ids_h.size} in-vocab, V={V}, {time.time() - t0:.1f}s")
+
+    # ---- host products (bit-exact restatements) + device residency -------------
+    t0 = time.time()
+    keep = host.sample_probs(counts_v, args.subsample)
+    bounds = host.table_bounds(counts_v, args.table_size) if neg > 0 else None
+    codes = points = coff = None
+    if mode["hs"]:
+        codes, points, coff = host.huffman(counts_v)
+    iters_total = args.warmup + args.steps
+    cfg = Config(word_dim=d, window=args.window, negative=neg, hs=mode["hs"], cbow=mode["cbow"],
+                 cbow_mean=True, iter=iters_total, init_alpha=0.025 if not mode["cbow"] else 0.05,
+                 min_alpha=2.5e-6, table_size=args.table_size, device=local)
+    tr = DeviceTrainer(cfg)
+    stream = torch.cuda.current_stream()
+    tr.set_stream(stream.cuda_stream)
+    tr.upload_vocab(keep, bounds, codes, points, coff)
+    pitch = (d + 31) // 32 * 32
+    gW = torch.Generator(device=dev)
+    gW.manual_seed(args.seed)  # identical initial replicas on every rank
+    W = torch.zeros(V, pitch, dtype=torch.float32, device=dev)
+    W[:, :d] = (torch.rand(V, d, generator=gW, device=dev) - 0.5) / d
+    Cm = torch.zeros(V, pitch, dtype=torch.float32, device=dev) if (neg > 0 or mode["cbow"]) else None
+    if Cm is not None and mode["cbow"] and mode["hs"]:
+        Cm[:, :d] = (torch.rand(V, d, generator=gW, device=dev) - 0.5) / d
+    S = torch.zeros(max(V - 1, 1), pitch, dtype=torch.float32, device=dev) if mode["hs"] else None
+    tr.bind_model(W.data_ptr(), Cm.data_ptr() if Cm is not None else None,
+                  S.data_ptr() if S is not None else None, pitch)
+    tr.upload_corpus(ids_h, soff_h, n_tok)
+    tr.set_rng(N.W2V_RNG_PHILOX, (args.seed << 32) | (rank + 1))
+    tr.set_schedule(N.W2V_SCHED_PARALLEL)
+    tr.set_progress(0)
+    torch.cuda.synchronize()
+    log(f"[bench] resident in HBM ({time.time() - t0:.1f}s)")
+
+    mats = [m for m in (W, Cm, S) if m is not None]
+
+    def step(epoch, evs=None):
+        if evs is not None:
+            evs[0].record(stream)
+        tr.train_epoch_async(epoch)
+        if evs is not None:
+            evs[1].record(stream)
+        if world > 1:
+            for m in mats:  # periodic model averaging over xGMI (RCCL)
+                dist.all_reduce(m, op=dist.ReduceOp.AVG)
+
+    for w in range(args.warmup):
+        step(w)
+    torch.cuda.synchronize()
+    st0 = tr.read_stats()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k, events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    st1 = tr.read_stats()
+    kern_ms = [a.elapsed_time(b) for a, b in events]
+    delta = {k: st1[k] - st0[k] for k in st1}
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        wsum = torch.tensor([delta["words"]], dtype=torch.int64, device=dev)
+        dist.all_reduce(wsum)
+        words_total = int(wsum.item())
+    else:
+        words_total = delta["words"]
+    for m in mats:
+        assert torch.isfinite(m).all().item(), "non-finite weights"
+
+    value = words_total / elapsed
+    # algorithmic HBM bytes per launch: fp32 rows read+written
+    if mode["cbow"]:
+        row_moves = 2 * delta["contexts"] + 2 * delta["targets"]
+    else:
+        row_moves = 2 * delta["centers"] + 2 * delta["targets"]
+    bytes_per_launch = (4 * d * row_moves + 4 * delta["draws"]) / args.steps
+    avg_kernel_s = float(np.mean(kern_ms)) / 1e3
+    achieved = bytes_per_launch / avg_kernel_s / 1e9
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, bytes_per_launch),
+                "kernel": "train_epoch_kernel", "avg_launch_ms": round(avg_kernel_s * 1e3, 3),
+                "algorithmic_bytes_per_launch": int(bytes_per_launch)}
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(args, counts_v, ids_h, soff_h, neg, mode)
+
+    if rank == 0:
+        out = {
+            "metric": "trained words/sec, dim=300 SGNS (per-GPU replica, RCCL model averaging for N>1)",
+            "value": round(value, 1),
+            "unit": "words/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{args.mode} neg{neg} d{d} w{args.window} subsample {args.subsample} min_count "
+                            f"{args.min_count}; synthetic Zipf(s=1) over {args.vocab} ranks standing in for 1B-Word "
+                            f"(configs[2]); {args.sent_len}-token sentences",
+                "tokens_per_gpu_per_step": n_tok,
+                "in_vocab_tokens_per_gpu_per_step": int(ids_h.size),
+                "vocab_size": V,
+                "global_batch": n_tok * world,
+                "parallelism": f"dp{world} (replicas + RCCL all-reduce average per step)" if world > 1 else "dp1",
+                "kept_centers_per_step": int(delta["centers"] / args.steps),
+                "targets_per_step": int(delta["targets"] / args.steps),
+            },
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    tr.close()
+
+
+def pmc_traffic(args, bytes_per_launch):
+    """HBM bytes per launch from a committed rocprofv3 PMC pass of this workload, if present."""
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    if not f.exists():
+        return None
+    try:
+        rec = json.loads(f.read_text())
+        key = f"{args.mode}_d{args.dim}_n{args.tokens}"
+        return rec.get(key)
+    except Exception:
+        return None
+
+
+def cpu_baseline(args, counts_v, ids_h, soff_h, neg, mode):
+    """The oracle's OpenMP restatement of the reference loop on the host cores,
+    over a bounded prefix of the same shard (same params)."""
+    from oracle import Oracle
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    o = Oracle(iter=1, window=args.window, min_count=args.min_count, table_size=args.table_size,
+               word_dim=args.dim, negative=neg, subsample_threshold=args.subsample, init_alpha=0.025,
+               min_alpha=2.5e-6, cbow_mean=True, train_method="hs" if mode["hs"] else "ns",
+               model="cbow" if mode["cbow"] else "sg")
+    o.set_vocab_counts(counts_v)
+    o.seed(args.seed)
+    # calibrate on a small prefix, then time a prefix sized to the budget
+    n_cal = 32
+    o.set_samples(ids_h[: soff_h[n_cal]], soff_h[: n_cal + 1], int(n_cal * args.sent_len))
+    o.init_weights()
+    t = time.perf_counter()
+    w = o.train_omp(threads, n_cal, 7)
+    rate = w / max(time.perf_counter() - t, 1e-6)
+    n = int(min(soff_h.size - 1, max(n_cal, rate * args.cpu_seconds / max(1, args.sent_len))))
+    o.set_samples(ids_h[: soff_h[n]], soff_h[: n + 1], int(n * args.sent_len))
+    t = time.perf_counter()
+    w = o.train_omp(threads, n, 11)
+    dt = time.perf_counter() - t
+    return {"value": round(w / dt, 1), "unit": "words/s", "cores": threads, "kind": "port",
+            "sample": f"{n} sentences ({w} in-vocab tokens) of the same shard, {dt:.1f}s, oracle OpenMP loop "
+                      f"(per-call hash map / set, static schedule, per-thread mt19937)"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,157 @@
+/*
+ * w2v_dev.h — the C-ABI drop-in boundary between the host Word2Vec class and
+ * the gfx950 (MI355X) training kernels.
+ *
+ * The reference (lache/word2vec) has no FFI: its hot path is the member
+ * functions of class Word2Vec (/root/reference/Word2Vec.h:29-90) running an
+ * OpenMP Hogwild loop over Eigen rows (Word2Vec.cpp:232-396). This header is
+ * the thin C layer that host code behind the same class API calls instead of
+ * that loop. Every entry point uses plain pointers and sizes (no C++/torch
+ * types), returns W2V_OK or an error code, never throws, and records a
+ * human-readable message retrievable with w2v_dev_last_error().
+ *
+ * Threading: one handle is used from one host thread at a time. Functions are
+ * synchronous unless their name ends in _async; _async work is ordered on the
+ * handle's HIP stream (w2v_dev_set_stream).
+ *
+ * Device layout (HBM): W, C and synapses1 are row-major fp32 with a row pitch
+ * of round_up(word_dim, 32) floats (128-B aligned rows); the unigram table is
+ * uint32[table_size]; sample probabilities fp32[V]; Huffman paths are CSR
+ * (uint8 codes, int32 points, int64 offsets); the corpus is int32 token ids
+ * with int64 sentence offsets.
+ */
+#ifndef W2V_DEV_H
+#define W2V_DEV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define W2V_OK 0
+#define W2V_ERR_ARG 1         /* invalid argument / size */
+#define W2V_ERR_HIP 2         /* a HIP runtime call failed */
+#define W2V_ERR_STATE 3       /* call out of order (e.g. train before upload) */
+#define W2V_ERR_UNSUPPORTED 4 /* configuration outside the kernels' range */
+
+/* RNG modes for the training kernels. */
+#define W2V_RNG_PHILOX 0 /* counter-based Philox4x32-10 per (epoch, sentence, position, slot, k) */
+#define W2V_RNG_REPLAY 1 /* consume a host-recorded stream in the reference's draw order */
+
+/* Schedules. */
+#define W2V_SCHED_PARALLEL 0   /* one wavefront per sentence, Hogwild across sentences */
+#define W2V_SCHED_SEQUENTIAL 1 /* one wavefront walks the sentences in order: deterministic */
+
+typedef struct w2v_dev w2v_dev; /* opaque handle */
+
+/* Mirrors the Word2Vec constructor arguments that shape the hot path
+ * (Word2Vec.h:64-66; members Word2Vec.h:32-46). */
+typedef struct w2v_dev_config {
+  int32_t word_dim;  /* Word2Vec::word_dim  (Word2Vec.h:36)                      */
+  int32_t window;    /* Word2Vec::window    (Word2Vec.h:33)                      */
+  int32_t negative;  /* Word2Vec::negative  (Word2Vec.h:37), 0 disables NS       */
+  int32_t hs;        /* train_method == "hs" (Word2Vec.cpp:162,206,342,304)       */
+  int32_t cbow;      /* model == "cbow"     (Word2Vec.cpp:387-390)               */
+  int32_t cbow_mean; /* Word2Vec::cbow_mean (Word2Vec.h:43)                      */
+  int32_t iter;      /* Word2Vec::iter      (Word2Vec.h:32), alpha schedule      */
+  float init_alpha;  /* Word2Vec::init_alpha (Word2Vec.h:39)                     */
+  float min_alpha;   /* Word2Vec::min_alpha  (Word2Vec.h:40)                     */
+  int64_t table_size;/* Word2Vec::table_size (Word2Vec.h:35)                     */
+  int32_t device;    /* HIP device ordinal; -1 = the calling thread's current    */
+  int32_t reserved;
+} w2v_dev_config;
+
+/* Counters accumulated by the kernels (reset with w2v_dev_reset_stats). */
+typedef struct w2v_dev_stats {
+  int64_t words;     /* in-vocab tokens consumed: the reference's current_words
+                        increments (Word2Vec.cpp:392-393)                        */
+  int64_t centers;   /* centers kept by subsampling (Word2Vec.cpp:282,332)       */
+  int64_t contexts;  /* SG: (center, context) pairs; CBOW: unique context rows   */
+  int64_t targets;   /* output rows updated: NS targets + HS path nodes          */
+  int64_t draws;     /* unigram-table draws (Word2Vec.cpp:255)                   */
+  int64_t sentences; /* sentences processed                                      */
+} w2v_dev_stats;
+
+/* Library / error. */
+const char* w2v_dev_version(void);
+const char* w2v_dev_last_error(void); /* thread-local message of the last failure */
+
+/* Replaces: the Word2Vec ctor's device-relevant state (Word2Vec.cpp:12-17). */
+int w2v_dev_create(const w2v_dev_config* cfg, w2v_dev** out);
+void w2v_dev_destroy(w2v_dev* h);
+
+/* Stream the handle enqueues on (a hipStream_t; NULL = a private stream). */
+int w2v_dev_set_stream(w2v_dev* h, void* hip_stream);
+/* RNG mode + Philox key. Replaces: generator/distribution members (Word2Vec.h:55-59). */
+int w2v_dev_set_rng(w2v_dev* h, int32_t rng_mode, uint64_t seed);
+int w2v_dev_set_schedule(w2v_dev* h, int32_t schedule);
+
+/* Replaces: the products of build_vocab (Word2Vec.cpp:132-169) consumed by the
+ * hot path — Word::sample_probability (precalc_sampling :115-130), the unigram
+ * table (make_table :81-113) given as V+1 first-index boundaries of the
+ * monotone table (NULL when negative == 0), and Word::codes/points
+ * (create_huffman_tree :32-79) as CSR (NULL when hs == 0). */
+int w2v_dev_upload_vocab(w2v_dev* h, int64_t vocab_size, const float* sample_probability,
+                         const int64_t* table_bounds, const uint8_t* codes,
+                         const int32_t* points, const int64_t* code_offsets);
+/* Alternative to table_bounds: the expanded table (Word2Vec.h:51), n == table_size. */
+int w2v_dev_upload_table(w2v_dev* h, const uint32_t* table, int64_t n);
+
+/* Replaces: the W / C / synapses1 members (Word2Vec.h:53) and init_weights'
+ * result (Word2Vec.cpp:198-210). Host arrays are dense rows of word_dim floats:
+ * W and C have V rows, synapses1 V-1. NULL skips a matrix. */
+int w2v_dev_upload_model(w2v_dev* h, const float* W, const float* C, const float* syn1);
+int w2v_dev_download_model(w2v_dev* h, float* W, float* C, float* syn1);
+/* Train on caller-owned device matrices instead (e.g. torch tensors that an
+ * RCCL all-reduce also touches): rows of `pitch` floats (pitch % 4 == 0,
+ * pitch >= word_dim, 16-B aligned bases), padding columns zero. NULL for a
+ * matrix the configuration does not use. The handle never frees them. */
+int w2v_dev_bind_model(w2v_dev* h, float* dW, float* dC, float* dsyn1, int64_t pitch);
+/* Device pointers and row pitch (floats) of the resident matrices, for
+ * collectives (RCCL model averaging) on the caller's side. */
+int w2v_dev_model_layout(w2v_dev* h, float** dW, float** dC, float** dsyn1, int64_t* pitch);
+
+/* Replaces: build_sample's vector<vector<Word*>> (Word2Vec.cpp:212-230) and
+ * train_words (:362-363, raw tokens incl. OOV, drives the alpha schedule). */
+int w2v_dev_upload_corpus(w2v_dev* h, const int32_t* ids, int64_t n_tokens,
+                          const int64_t* sent_offsets, int64_t n_sentences,
+                          int64_t train_words);
+/* Replay mode: recorded draws in the reference's order (u per token; window
+ * shrink per kept token; table positions per NS call) and their start offset
+ * per [epoch * n_sentences + sentence]. */
+int w2v_dev_upload_replay(w2v_dev* h, const uint32_t* stream, int64_t n,
+                          const int64_t* stream_offsets, int64_t n_offsets);
+
+/* The reference's shared current_words counter (Word2Vec.cpp:359,393). */
+int w2v_dev_set_progress(w2v_dev* h, int64_t current_words);
+int w2v_dev_get_progress(w2v_dev* h, int64_t* current_words);
+
+/* Replaces: one iteration of train()'s epoch loop (Word2Vec.cpp:371-395):
+ * the sentences are visited in `order` (host array of n_sentences sentence
+ * ids — the std::shuffle result; NULL = identity), alpha follows the
+ * reference schedule from the device progress counter, and every sentence is
+ * trained by train_sentence_sg/cbow semantics (:273-353). Synchronous; adds
+ * this epoch's counters to *stats when stats != NULL. */
+int w2v_dev_train_epoch(w2v_dev* h, int32_t epoch, const int64_t* order, w2v_dev_stats* stats);
+/* The same, enqueued on the handle's stream; `order_dev` is a device array or NULL. */
+int w2v_dev_train_epoch_async(w2v_dev* h, int32_t epoch, const int64_t* order_dev);
+int w2v_dev_synchronize(w2v_dev* h);
+int w2v_dev_read_stats(w2v_dev* h, w2v_dev_stats* stats); /* cumulative; synchronizes */
+int w2v_dev_reset_stats(w2v_dev* h);
+
+/* Replaces: negative_sampling / hierarchical_softmax called on their own
+ * (Word2Vec.cpp:232-271, public API Word2Vec.h:81-82). Applies, in order, the
+ * n target updates {row rows[t] of matrix `which` (0 = W, 1 = C, 2 =
+ * synapses1), code codes[t]} against input `x`, accumulating into `grad`
+ * (host arrays of word_dim floats; grad is read and written). hs_form selects
+ * the HS arithmetic (g = (1 - code - f) * alpha in double, :241-242) or the NS
+ * one (g = (label - f) * alpha with label = 1 - code, :263-264). */
+int w2v_dev_apply_targets(w2v_dev* h, int32_t which, const float* x, float* grad,
+                          const int64_t* rows, const uint8_t* codes, int32_t n, float alpha,
+                          int32_t hs_form);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* W2V_DEV_H */

@@ -1,0 +1,65 @@
+"""Shared setup: run the oracle, mirror its products onto the device C-ABI."""
+from __future__ import annotations
+
+import numpy as np
+
+from oracle import Oracle
+
+
+MODES = {
+    "sg_ns": dict(model="sg", train_method="ns", negative=5),
+    "sg_hs": dict(model="sg", train_method="hs", negative=0),
+    "cbow_ns": dict(model="cbow", train_method="ns", negative=5),
+    "cbow_hs": dict(model="cbow", train_method="hs", negative=0),
+}
+
+
+def oracle_run(sentences, mode: str, dim=32, window=5, iters=1, seed=1234, min_count=2,
+               table_size=100_000, subsample=1e-3, cbow_mean=True, init_alpha=0.05, min_alpha=2.5e-6,
+               train=True):
+    m = MODES[mode]
+    o = Oracle(iter=iters, window=window, min_count=min_count, table_size=table_size, word_dim=dim,
+               negative=m["negative"], subsample_threshold=subsample, init_alpha=init_alpha,
+               min_alpha=min_alpha, cbow_mean=cbow_mean, train_method=m["train_method"], model=m["model"])
+    o.load_sentences(sentences)
+    o.seed(seed)
+    o.build_vocab()
+    o.init_weights()  # main.cpp:190 — train() re-inits (Word2Vec.cpp:358)
+    if train:
+        o.train(record=True)
+    return o
+
+
+def device_config(o: Oracle, mode: str, dim, window, iters, table_size, cbow_mean, init_alpha, min_alpha):
+    from word2vec_amd.device import Config
+
+    m = MODES[mode]
+    return Config(word_dim=dim, window=window, negative=m["negative"], hs=m["train_method"] == "hs",
+                  cbow=m["model"] == "cbow", cbow_mean=cbow_mean, iter=iters, init_alpha=init_alpha,
+                  min_alpha=min_alpha, table_size=table_size)
+
+
+def device_from_oracle(o: Oracle, cfg, initial=True):
+    from word2vec_amd.device import DeviceTrainer
+
+    d = DeviceTrainer(cfg)
+    keep = o.sample_probs()
+    bounds = o.table_bounds() if cfg.negative > 0 else None
+    codes = points = off = None
+    if cfg.hs:
+        codes, points, off = o.huffman()
+    d.upload_vocab(keep, bounds, codes, points, off)
+    W = o.matrix(0, initial)
+    Cm = o.matrix(1, initial) if (cfg.negative > 0 or cfg.cbow) else None
+    S = o.matrix(2, initial) if cfg.hs else None
+    d.upload_model(W, Cm, S)
+    ids, soff = o.samples()
+    d.upload_corpus(ids, soff, o.train_words)
+    return d
+
+
+def rel_err(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    den = max(np.abs(b).max(), 1e-30)
+    return float(np.abs(a - b).max() / den)

@@ -1,0 +1,118 @@
+"""GPU parity: the HIP kernels (through the C-ABI) against the CPU oracle.
+
+Replay mode feeds the kernels the reference's own mt19937 draw stream (recorded
+by the oracle in the reference's order), so every subsampling decision, window
+shrink and negative is identical; the remaining difference is fp32 summation
+order (wave-tree dot products vs the oracle's sequential sum). Philox mode
+checks the throughput-mode RNG bit-for-bit and its arithmetic the same way.
+Tolerance: north_star's 1e-5 relative for a single deterministic update
+(one sentence); looser bounds for multi-sentence runs where rounding
+differences compound through repeated rows.
+"""
+import numpy as np
+import pytest
+
+from tests.corpus import zipf_sentences
+from tests.harness import MODES, device_config, device_from_oracle, oracle_run, rel_err
+
+pytestmark = pytest.mark.gpu
+
+from word2vec_amd import _native as N  # noqa: E402
+
+
+def _run_replay(mode, sentences, dim, window, iters, table_size=100_000, cbow_mean=True):
+    o = oracle_run(sentences, mode, dim=dim, window=window, iters=iters, table_size=table_size,
+                   cbow_mean=cbow_mean)
+    cfg = device_config(o, mode, dim, window, iters, table_size, cbow_mean, 0.05, 2.5e-6)
+    d = device_from_oracle(o, cfg, initial=True)
+    stream, offs, orders = o.stream(iters)
+    d.upload_replay(stream, offs)
+    d.set_rng(N.W2V_RNG_REPLAY, 0)
+    d.set_schedule(N.W2V_SCHED_SEQUENTIAL)
+    d.set_progress(0)
+    n = orders.size // iters
+    for e in range(iters):
+        d.train_epoch(e, orders[e * n:(e + 1) * n])
+    got = d.download_model()
+    want = (o.matrix(0), o.matrix(1) if cfg.negative > 0 or cfg.cbow else None, o.matrix(2) if cfg.hs else None)
+    init = (o.matrix(0, True), o.matrix(1, True) if want[1] is not None else None,
+            o.matrix(2, True) if want[2] is not None else None)
+    assert d.get_progress() == o.current_words
+    return got, want, init
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+def test_replay_single_sentence(mode):
+    sents = zipf_sentences(1, 120, 60, seed=3)
+    got, want, init = _run_replay(mode, sents, dim=48, window=5, iters=1, table_size=10_000)
+    for g, w, i in zip(got, want, init):
+        if w is None:
+            continue
+        dw = w - i
+        if np.abs(dw).max() == 0:
+            np.testing.assert_array_equal(g, w)
+            continue
+        assert rel_err(g - i, dw) < 1e-5, mode
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("dim", [100, 300])
+def test_replay_epoch(mode, dim):
+    sents = zipf_sentences(12, 200, 400, seed=5, ragged=True)
+    got, want, init = _run_replay(mode, sents, dim=dim, window=5, iters=2)
+    for g, w, i in zip(got, want, init):
+        if w is None:
+            continue
+        assert rel_err(g - i, w - i) < 1e-4, mode
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+def test_philox_sequential(mode):
+    sents = zipf_sentences(10, 150, 300, seed=9, ragged=True)
+    dim, window, iters, ts = 64, 5, 1, 100_000
+    o = oracle_run(sents, mode, dim=dim, window=window, iters=iters, table_size=ts, train=False)
+    o.build_sample()
+    cfg = device_config(o, mode, dim, window, iters, ts, True, 0.05, 2.5e-6)
+    d = device_from_oracle(o, cfg, initial=False)
+    init = [o.matrix(k) for k in range(3)]
+    key = 0x1234_5678_9ABC_DEF0
+    n = o.samples()[1].size - 1
+    order = np.random.default_rng(0).permutation(n)
+    o.train_philox(0, 1, order, key, 0)
+    d.set_rng(N.W2V_RNG_PHILOX, key)
+    d.set_schedule(N.W2V_SCHED_SEQUENTIAL)
+    d.set_progress(0)
+    st = d.train_epoch(0, order)
+    assert st["words"] == o.current_words
+    got = d.download_model()
+    for k, g in enumerate(got):
+        if g is None:
+            continue
+        w = o.matrix(k)
+        assert rel_err(g - init[k], w - init[k]) < 1e-4, (mode, k)
+
+
+@pytest.mark.parametrize("mode", ["sg_ns", "cbow_hs"])
+def test_parallel_runs_and_counts(mode):
+    sents = zipf_sentences(400, 300, 2000, seed=11, ragged=True)
+    dim = 300
+    o = oracle_run(sents, mode, dim=dim, window=5, iters=1, table_size=1_000_000, train=False)
+    o.build_sample()
+    cfg = device_config(o, mode, dim, 5, 1, 1_000_000, True, 0.05, 2.5e-6)
+    d = device_from_oracle(o, cfg, initial=False)
+    d.set_rng(N.W2V_RNG_PHILOX, 7)
+    d.set_schedule(N.W2V_SCHED_PARALLEL)
+    d.set_progress(0)
+    st = d.train_epoch(0, None)
+    ids, off = o.samples()
+    assert st["words"] == ids.size
+    assert st["sentences"] == off.size - 1
+    W, Cm, S = d.download_model()
+    for m in (W, Cm, S):
+        if m is not None:
+            assert np.isfinite(m).all()
+    # kept fraction matches E[min(p,1)] over tokens within a few sigma
+    p = o.sample_probs()[ids].astype(np.float64)
+    exp_kept = p.sum()
+    sd = np.sqrt((p * (1 - p)).sum()) + 1
+    assert abs(st["centers"] - exp_kept) < 6 * sd + (0 if mode.startswith("sg") else 0.01 * exp_kept)

@@ -1,0 +1,119 @@
+"""ctypes binding of the C-ABI in include/w2v_dev.h (libw2v_hip.so).
+
+The library is built in-tree (``word2vec_amd/lib``) by ``__graft_entry__.build()``
+or ``make -C word2vec_amd/csrc``. There is no fallback: if the HIP library is
+missing, importing the device API raises, so nothing can silently run a CPU
+path in its place.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+LIB_DIR = Path(__file__).resolve().parent / "lib"
+DEV_LIB = LIB_DIR / "libw2v_hip.so"
+
+W2V_OK = 0
+W2V_RNG_PHILOX = 0
+W2V_RNG_REPLAY = 1
+W2V_SCHED_PARALLEL = 0
+W2V_SCHED_SEQUENTIAL = 1
+
+
+class DevConfig(C.Structure):
+    _fields_ = [
+        ("word_dim", C.c_int32),
+        ("window", C.c_int32),
+        ("negative", C.c_int32),
+        ("hs", C.c_int32),
+        ("cbow", C.c_int32),
+        ("cbow_mean", C.c_int32),
+        ("iter", C.c_int32),
+        ("init_alpha", C.c_float),
+        ("min_alpha", C.c_float),
+        ("table_size", C.c_int64),
+        ("device", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+
+class DevStats(C.Structure):
+    _fields_ = [
+        ("words", C.c_int64),
+        ("centers", C.c_int64),
+        ("contexts", C.c_int64),
+        ("targets", C.c_int64),
+        ("draws", C.c_int64),
+        ("sentences", C.c_int64),
+    ]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+_P = C.c_void_p
+_I32 = C.c_int32
+_I64 = C.c_int64
+_U64 = C.c_uint64
+_F = C.c_float
+
+# name -> (restype, argtypes); mirrors include/w2v_dev.h one for one.
+SIGNATURES = {
+    "w2v_dev_version": (C.c_char_p, []),
+    "w2v_dev_last_error": (C.c_char_p, []),
+    "w2v_dev_create": (C.c_int, [C.POINTER(DevConfig), C.POINTER(_P)]),
+    "w2v_dev_destroy": (None, [_P]),
+    "w2v_dev_set_stream": (C.c_int, [_P, _P]),
+    "w2v_dev_set_rng": (C.c_int, [_P, _I32, _U64]),
+    "w2v_dev_set_schedule": (C.c_int, [_P, _I32]),
+    "w2v_dev_upload_vocab": (C.c_int, [_P, _I64, _P, _P, _P, _P, _P]),
+    "w2v_dev_upload_table": (C.c_int, [_P, _P, _I64]),
+    "w2v_dev_upload_model": (C.c_int, [_P, _P, _P, _P]),
+    "w2v_dev_download_model": (C.c_int, [_P, _P, _P, _P]),
+    "w2v_dev_bind_model": (C.c_int, [_P, _P, _P, _P, _I64]),
+    "w2v_dev_model_layout": (C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), C.POINTER(_I64)]),
+    "w2v_dev_upload_corpus": (C.c_int, [_P, _P, _I64, _P, _I64, _I64]),
+    "w2v_dev_upload_replay": (C.c_int, [_P, _P, _I64, _P, _I64]),
+    "w2v_dev_set_progress": (C.c_int, [_P, _I64]),
+    "w2v_dev_get_progress": (C.c_int, [_P, C.POINTER(_I64)]),
+    "w2v_dev_train_epoch": (C.c_int, [_P, _I32, _P, C.POINTER(DevStats)]),
+    "w2v_dev_train_epoch_async": (C.c_int, [_P, _I32, _P]),
+    "w2v_dev_synchronize": (C.c_int, [_P]),
+    "w2v_dev_read_stats": (C.c_int, [_P, C.POINTER(DevStats)]),
+    "w2v_dev_reset_stats": (C.c_int, [_P]),
+    "w2v_dev_apply_targets": (C.c_int, [_P, _I32, _P, _P, _P, _P, _I32, _F, _I32]),
+}
+
+_lib = None
+
+
+def load_dev_lib(path: os.PathLike | str | None = None) -> C.CDLL:
+    """Load libw2v_hip.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else DEV_LIB
+    if not p.exists():
+        raise RuntimeError(
+            f"word2vec_amd: HIP library {p} is missing; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` or `make -C word2vec_amd/csrc`"
+        )
+    lib = C.CDLL(str(p), mode=C.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+class DevError(RuntimeError):
+    pass
+
+
+def check(lib: C.CDLL, rc: int, what: str) -> None:
+    if rc != W2V_OK:
+        msg = lib.w2v_dev_last_error().decode(errors="replace")
+        raise DevError(f"{what} failed (code {rc}): {msg}")

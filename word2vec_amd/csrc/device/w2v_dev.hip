@@ -1,0 +1,580 @@
+// w2v_dev.hip — implementation of the C-ABI in include/w2v_dev.h: HBM
+// residency of the model / vocab products / corpus, and the launches of the
+// gfx950 kernels in w2v_kernels.hpp. No exceptions cross the boundary.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "w2v_dev.h"
+#include "w2v_kernels.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                \
+  do {                                                                               \
+    hipError_t e_ = (expr);                                                          \
+    if (e_ != hipSuccess)                                                            \
+      return fail(W2V_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
+  } while (0)
+
+template <class T>
+void dfree(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+}  // namespace
+
+struct w2v_dev {
+  w2v_dev_config cfg{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  int64_t V = 0;
+  int64_t pitch = 0;
+  int32_t d4 = 0;
+  int vpl = 1;
+  bool need_C = false, need_S = false;
+  float* W = nullptr;
+  float* C = nullptr;
+  float* S = nullptr;
+  float* keep = nullptr;
+  uint32_t* table = nullptr;
+  uint8_t* codes = nullptr;
+  int32_t* points = nullptr;
+  int64_t* coff = nullptr;
+  int64_t n_codes = 0;
+  int32_t* ids = nullptr;
+  int64_t* soff = nullptr;
+  int64_t n_tok = 0, n_sent = 0, train_words = 0;
+  int64_t* order = nullptr;
+  uint32_t* replay = nullptr;
+  int64_t* replay_off = nullptr;
+  int64_t n_replay_off = 0;
+  unsigned long long* counters = nullptr;  // [0] words, [1..5] stats
+  unsigned int* work = nullptr;
+  float* scratch_f = nullptr;      // x | grad for apply_targets
+  int64_t* scratch_rows = nullptr;
+  uint8_t* scratch_codes = nullptr;
+  int64_t scratch_n = 0;
+  int32_t rng = W2V_RNG_PHILOX;
+  uint64_t seed = 0;
+  int32_t sched = W2V_SCHED_PARALLEL;
+  int n_cu = 256;
+  bool model_ready = false, vocab_ready = false, corpus_ready = false;
+  bool model_bound = false;  // W/C/S owned by the caller
+};
+
+namespace {
+
+constexpr int kMaxT = 8;
+
+using KernelFn = void (*)(w2v::TrainArgs);
+
+template <int VPL>
+KernelFn pick_kernel(bool cbow, bool hs, bool ns, bool replay) {
+#define W2V_K(CB, H, N, R) &w2v::train_epoch_kernel<VPL, kMaxT, CB, H, N, R>
+#define W2V_KR(CB, H, N) (replay ? W2V_K(CB, H, N, true) : W2V_K(CB, H, N, false))
+  if (cbow) {
+    if (hs && ns) return W2V_KR(true, true, true);
+    if (hs) return W2V_KR(true, true, false);
+    return W2V_KR(true, false, true);
+  }
+  if (hs && ns) return W2V_KR(false, true, true);
+  if (hs) return W2V_KR(false, true, false);
+  return W2V_KR(false, false, true);
+#undef W2V_KR
+#undef W2V_K
+}
+
+KernelFn kernel_for(const w2v_dev* h) {
+  const bool cb = h->cfg.cbow != 0, hs = h->cfg.hs != 0, ns = h->cfg.negative > 0;
+  const bool rp = h->rng == W2V_RNG_REPLAY;
+  switch (h->vpl) {
+    case 1: return pick_kernel<1>(cb, hs, ns, rp);
+    case 2: return pick_kernel<2>(cb, hs, ns, rp);
+    case 3: return pick_kernel<3>(cb, hs, ns, rp);
+    default: return pick_kernel<4>(cb, hs, ns, rp);
+  }
+}
+
+int set_device(w2v_dev* h) {
+  HIP_TRY(hipSetDevice(h->device));
+  return W2V_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* w2v_dev_version(void) { return "word2vec_amd-dev 0.1 (gfx950)"; }
+const char* w2v_dev_last_error(void) { return g_err.c_str(); }
+
+int w2v_dev_create(const w2v_dev_config* cfg, w2v_dev** out) {
+  if (!cfg || !out) return fail(W2V_ERR_ARG, "w2v_dev_create: null argument");
+  *out = nullptr;
+  if (cfg->word_dim <= 0) return fail(W2V_ERR_ARG, "word_dim must be > 0");
+  if (cfg->word_dim > 1024) return fail(W2V_ERR_UNSUPPORTED, "word_dim > 1024 unsupported");
+  if (cfg->window < 0 || cfg->window > 31)
+    return fail(W2V_ERR_UNSUPPORTED, "window must be in [0, 31] (2*window+1 <= 64 lanes)");
+  if (cfg->negative < 0 || cfg->negative > 63)
+    return fail(W2V_ERR_UNSUPPORTED, "negative must be in [0, 63]");
+  if (!cfg->hs && cfg->negative == 0)
+    return fail(W2V_ERR_ARG, "neither hs nor negative sampling enabled");
+  if (cfg->negative > 0 && cfg->table_size <= 0) return fail(W2V_ERR_ARG, "table_size must be > 0");
+  if (cfg->iter <= 0) return fail(W2V_ERR_ARG, "iter must be > 0");
+  w2v_dev* h = new w2v_dev();
+  h->cfg = *cfg;
+  if (cfg->device >= 0) {
+    h->device = cfg->device;
+  } else {
+    hipError_t e = hipGetDevice(&h->device);
+    if (e != hipSuccess) {
+      delete h;
+      return fail(W2V_ERR_HIP, std::string("hipGetDevice: ") + hipGetErrorString(e));
+    }
+  }
+  hipError_t e = hipSetDevice(h->device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc(&h->counters, 8 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(h->counters, 0, 8 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc(&h->work, sizeof(unsigned int));
+  int ncu = 0;
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device);
+  if (e != hipSuccess) {
+    std::string msg = std::string("w2v_dev_create: ") + hipGetErrorString(e);
+    w2v_dev_destroy(h);
+    return fail(W2V_ERR_HIP, msg);
+  }
+  h->own_stream = true;
+  h->n_cu = ncu > 0 ? ncu : 256;
+  h->d4 = (cfg->word_dim + 3) & ~3;
+  h->pitch = (cfg->word_dim + 31) & ~31;
+  h->vpl = (h->d4 / 4 + w2v::kWave - 1) / w2v::kWave;
+  h->need_C = cfg->negative > 0 || cfg->cbow;
+  h->need_S = cfg->hs != 0;
+  *out = h;
+  return W2V_OK;
+}
+
+void w2v_dev_destroy(w2v_dev* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (!h->model_bound) { dfree(h->W); dfree(h->C); dfree(h->S); }
+  dfree(h->keep); dfree(h->table); dfree(h->codes); dfree(h->points); dfree(h->coff);
+  dfree(h->ids); dfree(h->soff); dfree(h->order); dfree(h->replay); dfree(h->replay_off);
+  dfree(h->counters); dfree(h->work);
+  dfree(h->scratch_f); dfree(h->scratch_rows); dfree(h->scratch_codes);
+  if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+int w2v_dev_set_stream(w2v_dev* h, void* s) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (set_device(h)) return W2V_ERR_HIP;
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  if (h->own_stream) HIP_TRY(hipStreamDestroy(h->stream));
+  if (s) {
+    h->stream = (hipStream_t)s;
+    h->own_stream = false;
+  } else {
+    HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    h->own_stream = true;
+  }
+  return W2V_OK;
+}
+
+int w2v_dev_set_rng(w2v_dev* h, int32_t mode, uint64_t seed) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (mode != W2V_RNG_PHILOX && mode != W2V_RNG_REPLAY) return fail(W2V_ERR_ARG, "bad rng mode");
+  h->rng = mode;
+  h->seed = seed;
+  return W2V_OK;
+}
+
+int w2v_dev_set_schedule(w2v_dev* h, int32_t s) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (s != W2V_SCHED_PARALLEL && s != W2V_SCHED_SEQUENTIAL) return fail(W2V_ERR_ARG, "bad schedule");
+  h->sched = s;
+  return W2V_OK;
+}
+
+int w2v_dev_upload_vocab(w2v_dev* h, int64_t V, const float* keep, const int64_t* bounds,
+                         const uint8_t* codes, const int32_t* points, const int64_t* coff) {
+  if (!h || !keep) return fail(W2V_ERR_ARG, "w2v_dev_upload_vocab: null argument");
+  if (V < 1 || V > (int64_t)INT32_MAX) return fail(W2V_ERR_ARG, "vocab_size out of range");
+  if (h->cfg.hs && V < 2) return fail(W2V_ERR_ARG, "hs needs vocab_size >= 2");
+  if (h->cfg.negative > 0 && !bounds && !h->table)
+    return fail(W2V_ERR_ARG, "negative sampling needs table_bounds (or w2v_dev_upload_table first)");
+  if (h->cfg.hs && (!codes || !points || !coff)) return fail(W2V_ERR_ARG, "hs needs codes/points/code_offsets");
+  if (set_device(h)) return W2V_ERR_HIP;
+  if (h->V != V) {
+    if (!h->model_bound) { dfree(h->W); dfree(h->C); dfree(h->S); }
+    h->W = h->C = h->S = nullptr;
+    h->model_bound = false;
+    h->pitch = (h->cfg.word_dim + 31) & ~31;
+    h->model_ready = false;
+  }
+  h->V = V;
+  dfree(h->keep);
+  HIP_TRY(hipMalloc(&h->keep, V * sizeof(float)));
+  HIP_TRY(hipMemcpy(h->keep, keep, V * sizeof(float), hipMemcpyHostToDevice));
+  if (h->cfg.negative > 0 && bounds) {
+    const int64_t n = h->cfg.table_size;
+    if (bounds[0] != 0 || bounds[V] != n) return fail(W2V_ERR_ARG, "table_bounds must start at 0 and end at table_size");
+    for (int64_t w = 0; w < V; ++w)
+      if (bounds[w] > bounds[w + 1]) return fail(W2V_ERR_ARG, "table_bounds must be non-decreasing");
+    int64_t* db = nullptr;
+    dfree(h->table);
+    HIP_TRY(hipMalloc(&h->table, n * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&db, (V + 1) * sizeof(int64_t)));
+    HIP_TRY(hipMemcpy(db, bounds, (V + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(w2v::expand_table_kernel, dim3(4096), dim3(256), 0, h->stream, db, V,
+                       h->table, n);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hipFree(db));
+  }
+  if (h->cfg.hs) {
+    for (int64_t w = 0; w < V; ++w)
+      if (coff[w] > coff[w + 1] || coff[w + 1] - coff[w] > 4096)
+        return fail(W2V_ERR_ARG, "code_offsets must be non-decreasing with paths <= 4096");
+    if (coff[0] != 0) return fail(W2V_ERR_ARG, "code_offsets[0] must be 0");
+    const int64_t nc = coff[V];
+    for (int64_t t = 0; t < nc; ++t)
+      if (points[t] < 0 || points[t] > V - 2 || codes[t] > 1)
+        return fail(W2V_ERR_ARG, "Huffman point/code out of range");
+    dfree(h->codes); dfree(h->points); dfree(h->coff);
+    HIP_TRY(hipMalloc(&h->codes, (nc > 0 ? nc : 1)));
+    HIP_TRY(hipMalloc(&h->points, (nc > 0 ? nc : 1) * sizeof(int32_t)));
+    HIP_TRY(hipMalloc(&h->coff, (V + 1) * sizeof(int64_t)));
+    if (nc > 0) {
+      HIP_TRY(hipMemcpy(h->codes, codes, nc, hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(h->points, points, nc * sizeof(int32_t), hipMemcpyHostToDevice));
+    }
+    HIP_TRY(hipMemcpy(h->coff, coff, (V + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+    h->n_codes = nc;
+  }
+  h->vocab_ready = true;
+  return W2V_OK;
+}
+
+int w2v_dev_upload_table(w2v_dev* h, const uint32_t* table, int64_t n) {
+  if (!h || !table) return fail(W2V_ERR_ARG, "w2v_dev_upload_table: null argument");
+  if (n != h->cfg.table_size) return fail(W2V_ERR_ARG, "table length != table_size");
+  if (set_device(h)) return W2V_ERR_HIP;
+  dfree(h->table);
+  HIP_TRY(hipMalloc(&h->table, n * sizeof(uint32_t)));
+  HIP_TRY(hipMemcpy(h->table, table, n * sizeof(uint32_t), hipMemcpyHostToDevice));
+  return W2V_OK;
+}
+
+static int ensure_model(w2v_dev* h) {
+  if (h->V < 1) return fail(W2V_ERR_STATE, "upload the vocab before the model");
+  const size_t rows_bytes = (size_t)h->V * h->pitch * sizeof(float);
+  if (!h->W) {
+    HIP_TRY(hipMalloc(&h->W, rows_bytes));
+    HIP_TRY(hipMemset(h->W, 0, rows_bytes));
+  }
+  if (h->need_C && !h->C) {
+    HIP_TRY(hipMalloc(&h->C, rows_bytes));
+    HIP_TRY(hipMemset(h->C, 0, rows_bytes));
+  }
+  if (h->need_S && !h->S) {
+    const size_t sb = (size_t)(h->V > 1 ? h->V - 1 : 1) * h->pitch * sizeof(float);
+    HIP_TRY(hipMalloc(&h->S, sb));
+    HIP_TRY(hipMemset(h->S, 0, sb));
+  }
+  return W2V_OK;
+}
+
+int w2v_dev_upload_model(w2v_dev* h, const float* W, const float* C, const float* S) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (set_device(h)) return W2V_ERR_HIP;
+  int rc = ensure_model(h);
+  if (rc) return rc;
+  const size_t d = (size_t)h->cfg.word_dim, dp = (size_t)h->pitch * sizeof(float);
+  if (W) HIP_TRY(hipMemcpy2D(h->W, dp, W, d * sizeof(float), d * sizeof(float), h->V, hipMemcpyHostToDevice));
+  if (C) {
+    if (!h->C) return fail(W2V_ERR_ARG, "C is not used by this configuration");
+    HIP_TRY(hipMemcpy2D(h->C, dp, C, d * sizeof(float), d * sizeof(float), h->V, hipMemcpyHostToDevice));
+  }
+  if (S) {
+    if (!h->S) return fail(W2V_ERR_ARG, "synapses1 is not used by this configuration");
+    if (h->V > 1)
+      HIP_TRY(hipMemcpy2D(h->S, dp, S, d * sizeof(float), d * sizeof(float), h->V - 1, hipMemcpyHostToDevice));
+  }
+  h->model_ready = true;
+  return W2V_OK;
+}
+
+int w2v_dev_download_model(w2v_dev* h, float* W, float* C, float* S) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (!h->W) return fail(W2V_ERR_STATE, "no model on the device");
+  if (set_device(h)) return W2V_ERR_HIP;
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  const size_t d = (size_t)h->cfg.word_dim, dp = (size_t)h->pitch * sizeof(float);
+  if (W) HIP_TRY(hipMemcpy2D(W, d * sizeof(float), h->W, dp, d * sizeof(float), h->V, hipMemcpyDeviceToHost));
+  if (C && h->C) HIP_TRY(hipMemcpy2D(C, d * sizeof(float), h->C, dp, d * sizeof(float), h->V, hipMemcpyDeviceToHost));
+  if (S && h->S && h->V > 1)
+    HIP_TRY(hipMemcpy2D(S, d * sizeof(float), h->S, dp, d * sizeof(float), h->V - 1, hipMemcpyDeviceToHost));
+  return W2V_OK;
+}
+
+int w2v_dev_bind_model(w2v_dev* h, float* dW, float* dC, float* dS, int64_t pitch) {
+  if (!h || !dW) return fail(W2V_ERR_ARG, "w2v_dev_bind_model: null argument");
+  if (h->V < 1) return fail(W2V_ERR_STATE, "upload the vocab before binding the model");
+  if (pitch < h->d4 || pitch % 4 != 0) return fail(W2V_ERR_ARG, "pitch must be >= word_dim rounded to 4 and a multiple of 4");
+  if (h->need_C && !dC) return fail(W2V_ERR_ARG, "this configuration needs C");
+  if (h->need_S && !dS) return fail(W2V_ERR_ARG, "this configuration needs synapses1");
+  for (const float* p : {dW, dC, dS})
+    if (p && (reinterpret_cast<uintptr_t>(p) & 15u)) return fail(W2V_ERR_ARG, "matrix base must be 16-B aligned");
+  if (!h->model_bound) { dfree(h->W); dfree(h->C); dfree(h->S); }
+  h->W = dW;
+  h->C = h->need_C ? dC : nullptr;
+  h->S = h->need_S ? dS : nullptr;
+  h->pitch = pitch;
+  h->model_bound = true;
+  h->model_ready = true;
+  return W2V_OK;
+}
+
+int w2v_dev_model_layout(w2v_dev* h, float** dW, float** dC, float** dS, int64_t* pitch) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (set_device(h)) return W2V_ERR_HIP;
+  int rc = ensure_model(h);
+  if (rc) return rc;
+  if (dW) *dW = h->W;
+  if (dC) *dC = h->C;
+  if (dS) *dS = h->S;
+  if (pitch) *pitch = h->pitch;
+  return W2V_OK;
+}
+
+int w2v_dev_upload_corpus(w2v_dev* h, const int32_t* ids, int64_t n_tok, const int64_t* soff,
+                          int64_t n_sent, int64_t train_words) {
+  if (!h || !soff || (n_tok > 0 && !ids)) return fail(W2V_ERR_ARG, "w2v_dev_upload_corpus: null argument");
+  if (n_sent < 0 || n_tok < 0 || n_sent > (int64_t)UINT32_MAX - 1)
+    return fail(W2V_ERR_ARG, "corpus sizes out of range");
+  if (soff[0] != 0 || soff[n_sent] != n_tok) return fail(W2V_ERR_ARG, "sentence offsets must span [0, n_tokens]");
+  for (int64_t s = 0; s < n_sent; ++s)
+    if (soff[s] > soff[s + 1] || soff[s + 1] - soff[s] > (int64_t)INT32_MAX)
+      return fail(W2V_ERR_ARG, "sentence offsets must be non-decreasing");
+  if (h->V < 1) return fail(W2V_ERR_STATE, "upload the vocab before the corpus");
+  for (int64_t t = 0; t < n_tok; ++t)
+    if (ids[t] < 0 || ids[t] >= h->V) return fail(W2V_ERR_ARG, "token id out of vocab range");
+  if (train_words <= 0 && n_tok > 0) return fail(W2V_ERR_ARG, "train_words must be > 0");
+  if (set_device(h)) return W2V_ERR_HIP;
+  dfree(h->ids); dfree(h->soff); dfree(h->order);
+  HIP_TRY(hipMalloc(&h->ids, (n_tok > 0 ? n_tok : 1) * sizeof(int32_t)));
+  if (n_tok > 0) HIP_TRY(hipMemcpy(h->ids, ids, n_tok * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&h->soff, (n_sent + 1) * sizeof(int64_t)));
+  HIP_TRY(hipMemcpy(h->soff, soff, (n_sent + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&h->order, (n_sent > 0 ? n_sent : 1) * sizeof(int64_t)));
+  h->n_tok = n_tok;
+  h->n_sent = n_sent;
+  h->train_words = train_words;
+  h->corpus_ready = true;
+  return W2V_OK;
+}
+
+int w2v_dev_upload_replay(w2v_dev* h, const uint32_t* stream, int64_t n, const int64_t* off,
+                          int64_t n_off) {
+  if (!h || !off || (n > 0 && !stream)) return fail(W2V_ERR_ARG, "w2v_dev_upload_replay: null argument");
+  for (int64_t k = 0; k < n_off; ++k)
+    if (off[k] < 0 || off[k] > n) return fail(W2V_ERR_ARG, "replay offset out of range");
+  if (set_device(h)) return W2V_ERR_HIP;
+  dfree(h->replay); dfree(h->replay_off);
+  HIP_TRY(hipMalloc(&h->replay, (n > 0 ? n : 1) * sizeof(uint32_t)));
+  if (n > 0) HIP_TRY(hipMemcpy(h->replay, stream, n * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&h->replay_off, (n_off > 0 ? n_off : 1) * sizeof(int64_t)));
+  if (n_off > 0) HIP_TRY(hipMemcpy(h->replay_off, off, n_off * sizeof(int64_t), hipMemcpyHostToDevice));
+  h->n_replay_off = n_off;
+  return W2V_OK;
+}
+
+int w2v_dev_set_progress(w2v_dev* h, int64_t cw) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (set_device(h)) return W2V_ERR_HIP;
+  unsigned long long v = (unsigned long long)cw;
+  HIP_TRY(hipMemcpyAsync(h->counters, &v, sizeof(v), hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return W2V_OK;
+}
+
+int w2v_dev_get_progress(w2v_dev* h, int64_t* cw) {
+  if (!h || !cw) return fail(W2V_ERR_ARG, "null argument");
+  if (set_device(h)) return W2V_ERR_HIP;
+  unsigned long long v = 0;
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hipMemcpy(&v, h->counters, sizeof(v), hipMemcpyDeviceToHost));
+  *cw = (int64_t)v;
+  return W2V_OK;
+}
+
+int w2v_dev_train_epoch_async(w2v_dev* h, int32_t epoch, const int64_t* order_dev) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (!h->vocab_ready || !h->corpus_ready) return fail(W2V_ERR_STATE, "upload vocab and corpus first");
+  if (!h->model_ready) return fail(W2V_ERR_STATE, "upload the model first");
+  if (h->cfg.negative > 0 && !h->table) return fail(W2V_ERR_STATE, "no unigram table on the device");
+  if (h->rng == W2V_RNG_REPLAY) {
+    if (!h->replay) return fail(W2V_ERR_STATE, "replay mode without a replay stream");
+    if ((int64_t)(epoch + 1) * h->n_sent > h->n_replay_off)
+      return fail(W2V_ERR_ARG, "replay offsets do not cover this epoch");
+  }
+  if (epoch < 0) return fail(W2V_ERR_ARG, "epoch must be >= 0");
+  if (h->n_sent == 0) return W2V_OK;
+  if (set_device(h)) return W2V_ERR_HIP;
+  w2v::TrainArgs a;
+  a.W = h->W; a.C = h->C; a.S = h->S;
+  a.pitch = h->pitch; a.d4 = h->d4;
+  a.window = h->cfg.window; a.negative = h->cfg.negative; a.cbow_mean = h->cfg.cbow_mean;
+  a.iter = h->cfg.iter; a.init_alpha = h->cfg.init_alpha; a.min_alpha = h->cfg.min_alpha;
+  a.train_words = (double)h->train_words;
+  a.ids = h->ids; a.soff = h->soff; a.order = order_dev; a.n_sent = h->n_sent;
+  a.keep = h->keep; a.table = h->table; a.table_size = h->cfg.table_size;
+  a.codes = h->codes; a.points = h->points; a.coff = h->coff;
+  a.replay = h->replay;
+  a.replay_off = h->replay_off ? h->replay_off + (int64_t)epoch * h->n_sent : nullptr;
+  a.words = h->counters;
+  a.work = h->work;
+  a.stats = h->counters + 1;
+  a.key0 = (uint32_t)h->seed; a.key1 = (uint32_t)(h->seed >> 32);
+  a.epoch = (uint32_t)epoch;
+  KernelFn fn = kernel_for(h);
+  HIP_TRY(hipMemsetAsync(h->work, 0, sizeof(unsigned int), h->stream));
+  dim3 grid(1), block(64);
+  if (h->sched == W2V_SCHED_PARALLEL) {
+    int per_cu = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0));
+    if (per_cu < 1) per_cu = 1;
+    const int64_t resident = (int64_t)per_cu * h->n_cu;
+    const int64_t need = (h->n_sent + 3) / 4;
+    grid = dim3((unsigned)(need < resident ? need : resident));
+    block = dim3(256);
+  }
+  hipLaunchKernelGGL(fn, grid, block, 0, h->stream, a);
+  HIP_TRY(hipGetLastError());
+  return W2V_OK;
+}
+
+int w2v_dev_train_epoch(w2v_dev* h, int32_t epoch, const int64_t* order, w2v_dev_stats* st) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  w2v_dev_stats before{};
+  if (st) {
+    int rc = w2v_dev_read_stats(h, &before);
+    if (rc) return rc;
+  }
+  const int64_t* od = nullptr;
+  if (order) {
+    for (int64_t k = 0; k < h->n_sent; ++k)
+      if (order[k] < 0 || order[k] >= h->n_sent) return fail(W2V_ERR_ARG, "order entry out of range");
+    if (set_device(h)) return W2V_ERR_HIP;
+    HIP_TRY(hipMemcpyAsync(h->order, order, h->n_sent * sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
+    od = h->order;
+  }
+  int rc = w2v_dev_train_epoch_async(h, epoch, od);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  if (st) {
+    w2v_dev_stats after{};
+    rc = w2v_dev_read_stats(h, &after);
+    if (rc) return rc;
+    st->words += after.words - before.words;
+    st->centers += after.centers - before.centers;
+    st->contexts += after.contexts - before.contexts;
+    st->targets += after.targets - before.targets;
+    st->draws += after.draws - before.draws;
+    st->sentences += after.sentences - before.sentences;
+  }
+  return W2V_OK;
+}
+
+int w2v_dev_synchronize(w2v_dev* h) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (set_device(h)) return W2V_ERR_HIP;
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return W2V_OK;
+}
+
+int w2v_dev_read_stats(w2v_dev* h, w2v_dev_stats* st) {
+  if (!h || !st) return fail(W2V_ERR_ARG, "null argument");
+  if (set_device(h)) return W2V_ERR_HIP;
+  unsigned long long c[8];
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hipMemcpy(c, h->counters, sizeof(c), hipMemcpyDeviceToHost));
+  st->words = (int64_t)c[0];
+  st->centers = (int64_t)c[1];
+  st->contexts = (int64_t)c[2];
+  st->targets = (int64_t)c[3];
+  st->draws = (int64_t)c[4];
+  st->sentences = (int64_t)c[5];
+  return W2V_OK;
+}
+
+int w2v_dev_reset_stats(w2v_dev* h) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (set_device(h)) return W2V_ERR_HIP;
+  HIP_TRY(hipMemsetAsync(h->counters + 1, 0, 7 * sizeof(unsigned long long), h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return W2V_OK;
+}
+
+int w2v_dev_apply_targets(w2v_dev* h, int32_t which, const float* x, float* grad,
+                          const int64_t* rows, const uint8_t* codes, int32_t n, float alpha,
+                          int32_t hs_form) {
+  if (!h || !x || !grad || (n > 0 && (!rows || !codes))) return fail(W2V_ERR_ARG, "null argument");
+  if (n < 0) return fail(W2V_ERR_ARG, "n < 0");
+  if (!h->model_ready) return fail(W2V_ERR_STATE, "upload the model first");
+  float* M = which == 0 ? h->W : which == 1 ? h->C : which == 2 ? h->S : nullptr;
+  if (!M) return fail(W2V_ERR_ARG, "matrix not resident for this configuration");
+  const int64_t rows_max = which == 2 ? h->V - 1 : h->V;
+  for (int32_t t = 0; t < n; ++t)
+    if (rows[t] < 0 || rows[t] >= rows_max) return fail(W2V_ERR_ARG, "row out of range");
+  if (set_device(h)) return W2V_ERR_HIP;
+  if (h->scratch_n < n || !h->scratch_f) {
+    dfree(h->scratch_f); dfree(h->scratch_rows); dfree(h->scratch_codes);
+    const int64_t cap = n > 64 ? n : 64;
+    HIP_TRY(hipMalloc(&h->scratch_f, 2 * (size_t)h->pitch * sizeof(float)));
+    HIP_TRY(hipMalloc(&h->scratch_rows, cap * sizeof(int64_t)));
+    HIP_TRY(hipMalloc(&h->scratch_codes, cap));
+    h->scratch_n = cap;
+  }
+  const size_t d = (size_t)h->cfg.word_dim;
+  float* dx = h->scratch_f;
+  float* dg = h->scratch_f + h->pitch;
+  HIP_TRY(hipMemsetAsync(h->scratch_f, 0, 2 * (size_t)h->pitch * sizeof(float), h->stream));
+  HIP_TRY(hipMemcpyAsync(dx, x, d * sizeof(float), hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(dg, grad, d * sizeof(float), hipMemcpyHostToDevice, h->stream));
+  if (n > 0) {
+    HIP_TRY(hipMemcpyAsync(h->scratch_rows, rows, n * sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipMemcpyAsync(h->scratch_codes, codes, n, hipMemcpyHostToDevice, h->stream));
+  }
+  void (*fn)(float*, int64_t, int, const float*, float*, const int64_t*, const uint8_t*, int, float, int);
+  switch (h->vpl) {
+    case 1: fn = &w2v::apply_targets_kernel<1>; break;
+    case 2: fn = &w2v::apply_targets_kernel<2>; break;
+    case 3: fn = &w2v::apply_targets_kernel<3>; break;
+    default: fn = &w2v::apply_targets_kernel<4>; break;
+  }
+  hipLaunchKernelGGL(fn, dim3(1), dim3(64), 0, h->stream, M, h->pitch, h->d4, dx, dg,
+                     h->scratch_rows, h->scratch_codes, n, alpha, hs_form);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(grad, dg, d * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return W2V_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,578 @@
+// w2v_kernels.hpp — gfx950 (CDNA4) training kernels for the Word2Vec hot path.
+//
+// What they compute is the reference's per-sentence update, unchanged:
+//   skip-gram  Word2Vec.cpp:319-353 (center W row is the input, fixed over the
+//              window; each context word is predicted; W[center] += grad once)
+//   CBOW       Word2Vec.cpp:273-317 (sum of C rows over the SET of context ids,
+//              /n if cbow_mean; scatter grad back to every unique id)
+//   NS         Word2Vec.cpp:251-271 (unique negatives from the unigram table,
+//              the positive overrides a colliding negative)
+//   HS         Word2Vec.cpp:232-249 (walk the Huffman path of the predicted word)
+// and the epoch loop Word2Vec.cpp:371-395 (sentences in the shuffled order,
+// alpha recomputed from the shared word counter every 10th sentence).
+//
+// How they map to MI355X:
+//   * one 64-lane wavefront owns one sentence at a time and walks it in order,
+//     exactly like one OpenMP thread of the reference; wavefronts dequeue
+//     sentences from a global head counter (Hogwild across sentences, as the
+//     reference is across threads). A one-wave grid is the deterministic
+//     sequential schedule used for parity.
+//   * an embedding row is spread over the wave as float4 lanes (lane l holds
+//     elements 4l..4l+3, 4(l+64)..): every row gather/scatter is one or a few
+//     fully coalesced 1-KiB wave instructions; the rows of all targets of one
+//     context (<= MAXT) are gathered together for memory-level parallelism.
+//   * dot products reduce across the wave with DPP (row rotations + row
+//     broadcasts, no LDS), the result read back with v_readlane into an SGPR,
+//     so the sigmoid and gradient scalar are wave-uniform.
+//   * axpy scatter-back is plain (lock-free, Hogwild) 16-B stores.
+//   * Philox4x32-10 counter-based draws make every random decision a pure
+//     function of (key, epoch, sentence, position, slot, k), so the parallel
+//     schedule needs no shared generator; in Philox mode subsampling decisions
+//     for 64 tokens are made at once (one lane per token) and only kept centers
+//     are walked. Replay mode instead consumes the reference's own mt19937
+//     stream recorded on the host, in the reference's draw order.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace w2v {
+
+constexpr int kWave = 64;
+
+struct TrainArgs {
+  float* W;
+  float* C;
+  float* S;             // synapses1
+  int64_t pitch;        // row pitch in floats (multiple of 32)
+  int32_t d4;           // word_dim rounded up to a multiple of 4
+  int32_t window;
+  int32_t negative;
+  int32_t cbow_mean;
+  int32_t iter;
+  float init_alpha;
+  float min_alpha;
+  double train_words;
+  const int32_t* ids;
+  const int64_t* soff;
+  const int64_t* order;  // may be null (identity)
+  int64_t n_sent;
+  const float* keep;
+  const uint32_t* table;
+  int64_t table_size;
+  const uint8_t* codes;
+  const int32_t* points;
+  const int64_t* coff;
+  const uint32_t* replay;      // replay stream
+  const int64_t* replay_off;   // per sentence, this epoch
+  unsigned long long* words;   // progress (current_words)
+  unsigned int* work;          // dequeue head
+  unsigned long long* stats;   // centers, contexts, targets, draws, sentences
+  uint32_t key0, key1, epoch;
+};
+
+struct Counters {
+  unsigned long long centers = 0, contexts = 0, targets = 0, draws = 0, sentences = 0;
+};
+
+// ---------------------------------------------------------------------------
+// Wave primitives
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+
+// Full-wave sum, broadcast to every lane (all 64 lanes must be active).
+__device__ __forceinline__ float wave_sum(float v) {
+  v += dpp_f<0xb1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4e>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x124>(v);  // row_ror:4
+  v += dpp_f<0x128>(v);  // row_ror:8
+  v += dpp_f<0x142>(v);  // row_bcast:15
+  v += dpp_f<0x143>(v);  // row_bcast:31
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+__device__ __forceinline__ int readlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ int uniform_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al. SC'11), the throughput-mode RNG.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                       uint32_t k0, uint32_t k1, uint32_t& o0, uint32_t& o1,
+                                       uint32_t& o2, uint32_t& o3) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  o0 = c0; o1 = c1; o2 = c2; o3 = c3;
+}
+
+// libstdc++ generate_canonical<float,24> of one 32-bit draw.
+__device__ __forceinline__ float canonical_f(uint32_t x) {
+  float r = (float)x * (1.0f / 4294967296.0f);
+  return r >= 1.0f ? __int_as_float(0x3F7FFFFF) : r;
+}
+
+__device__ __forceinline__ uint32_t philox_table_pos(const TrainArgs& a, uint32_t s, uint32_t i,
+                                                     uint32_t slot, uint32_t k) {
+  uint32_t o0, o1, o2, o3;
+  philox(i, s, (slot << 8) | k, a.epoch, a.key0, a.key1, o0, o1, o2, o3);
+  const uint64_t x = ((uint64_t)o1 << 32) | o0;
+  return (uint32_t)__umul64hi(x, (uint64_t)a.table_size);
+}
+
+// ---------------------------------------------------------------------------
+// Row I/O: a row is VPL float4 per lane, element 4*(lane + 64 v).
+// ---------------------------------------------------------------------------
+template <int VPL>
+__device__ __forceinline__ void load_row(const float* M, int64_t row, int64_t pitch, int d4,
+                                         int lane, float4 (&r)[VPL]) {
+  const float* p = M + row * pitch;
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int e = 4 * (lane + kWave * v);
+    r[v] = (e < d4) ? *reinterpret_cast<const float4*>(p + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+template <int VPL>
+__device__ __forceinline__ void store_row(float* M, int64_t row, int64_t pitch, int d4, int lane,
+                                          const float4 (&r)[VPL]) {
+  float* p = M + row * pitch;
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int e = 4 * (lane + kWave * v);
+    if (e < d4) *reinterpret_cast<float4*>(p + e) = r[v];
+  }
+}
+
+__device__ __forceinline__ float dot4(const float4 a, const float4 b) {
+  float s = a.x * b.x;
+  s += a.y * b.y;
+  s += a.z * b.z;
+  s += a.w * b.w;
+  return s;
+}
+
+__device__ __forceinline__ void axpy4(float4& y, float g, const float4 x) {
+  y.x += g * x.x;
+  y.y += g * x.y;
+  y.z += g * x.z;
+  y.w += g * x.w;
+}
+
+// ---------------------------------------------------------------------------
+// The per-target update (Word2Vec.cpp:238-246 HS; :261-268 NS), for up to
+// MAXT distinct rows at once. Lane (t0 + t) of row_l / code_l holds target t's
+// row and code (HS: Huffman code; NS: 1 - label). Rows are gathered together,
+// then updated in target order so grad accumulates in the reference's order.
+// ---------------------------------------------------------------------------
+template <int VPL, int MAXT, bool HSF>
+__device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d4, int lane, int T,
+                                              int row_l, int code_l, int t0,
+                                              const float4 (&x)[VPL], float4 (&g)[VPL],
+                                              float alpha) {
+  float4 r[MAXT][VPL];
+  int rows[MAXT];
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    rows[t] = readlane_i(row_l, t0 + t);
+    if (t < T) load_row<VPL>(M, rows[t], pitch, d4, lane, r[t]);
+  }
+  float f[MAXT];
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    f[t] = 0.f;
+    if (t < T) {
+      float p = 0.f;
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) p += dot4(r[t][v], x[v]);
+      f[t] = wave_sum(p);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    if (t < T) {
+      const int code = readlane_i(code_l, t0 + t);
+      const float e = expf(-f[t]);
+      float gt;
+      if (HSF) {
+        const float s = (float)(1.0 / (1.0 + (double)e));
+        gt = (float)((1.0 - (double)code - (double)s) * (double)alpha);
+      } else {
+        const float s = (float)(1.0 / (double)(1.0f + e));
+        gt = ((float)(1 - code) - s) * alpha;
+      }
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) {
+        axpy4(g[v], gt, r[t][v]);
+        axpy4(r[t][v], gt, x[v]);
+      }
+      store_row<VPL>(M, rows[t], pitch, d4, lane, r[t]);
+    }
+  }
+}
+
+// HS on the path of `word` (synapses1 rows).
+template <int VPL, int MAXT>
+__device__ __forceinline__ void hs_word(const TrainArgs& a, int word, int lane,
+                                        const float4 (&x)[VPL], float4 (&g)[VPL], float alpha,
+                                        Counters& cnt) {
+  const int64_t cb = a.coff[word];
+  const int L = (int)(a.coff[word + 1] - cb);
+  for (int c0 = 0; c0 < L; c0 += kWave) {
+    const int rem = min(kWave, L - c0);
+    const int pt_l = (lane < rem) ? a.points[cb + c0 + lane] : 0;
+    const int cd_l = (lane < rem) ? (int)a.codes[cb + c0 + lane] : 0;
+    for (int t0 = 0; t0 < rem; t0 += MAXT)
+      apply_targets<VPL, MAXT, true>(a.S, a.pitch, a.d4, lane, min(MAXT, rem - t0), pt_l, cd_l,
+                                     t0, x, g, alpha);
+    cnt.targets += (unsigned long long)rem;
+  }
+}
+
+// NS with positive `word` against `negw_l` lanes [base, base + neg): builds the
+// target list (positive first, then first occurrences of the negatives that
+// differ from it — the set semantics of Word2Vec.cpp:253-257) and applies it.
+template <int VPL, int MAXT>
+__device__ __forceinline__ void ns_word(const TrainArgs& a, float* M, int word, int negw_l,
+                                        int base, int lane, const float4 (&x)[VPL],
+                                        float4 (&g)[VPL], float alpha, Counters& cnt) {
+  const int neg = a.negative;
+  const int nk = __shfl(negw_l, (base + lane) & (kWave - 1));
+  bool dup = (lane >= neg) || (nk == word);
+  for (int j = 0; j < neg - 1; ++j) {
+    const int v = readlane_i(nk, j);
+    dup = dup || (lane > j && nk == v);
+  }
+  unsigned long long uniq = ballot(!dup);
+  int tgt_l = (lane == 0) ? word : 0;
+  int m = 1;
+  while (uniq) {
+    const int b = __builtin_ctzll(uniq);
+    uniq &= uniq - 1;
+    const int v = readlane_i(nk, b);
+    if (lane == m) tgt_l = v;
+    ++m;
+  }
+  const int T = m;
+  const int code_l = (lane == 0) ? 0 : 1;
+  for (int t0 = 0; t0 < T; t0 += MAXT)
+    apply_targets<VPL, MAXT, false>(M, a.pitch, a.d4, lane, min(MAXT, T - t0), tgt_l, code_l, t0,
+                                    x, g, alpha);
+  cnt.targets += (unsigned long long)T;
+}
+
+// Draw table words for `cnt_draws` (slot, k) pairs starting at slot `slot0`:
+// lane t -> slot0 + t / neg, k = t % neg.
+template <bool REPLAY>
+__device__ __forceinline__ int draw_negatives(const TrainArgs& a, uint32_t s, uint32_t i,
+                                              int slot0, int ndraw, int lane,
+                                              const uint32_t*& rp) {
+  int w = 0;
+  if (lane < ndraw) {
+    uint32_t pos;
+    if (REPLAY) {
+      pos = rp[lane];
+    } else {
+      const int neg = a.negative;
+      pos = philox_table_pos(a, s, i, (uint32_t)(slot0 + lane / neg), (uint32_t)(lane % neg));
+    }
+    w = (int)a.table[pos];
+  }
+  if (REPLAY) rp += ndraw;
+  return w;
+}
+
+// ---------------------------------------------------------------------------
+// Skip-gram center (Word2Vec.cpp:329-351) with its window [lo, hi).
+// ---------------------------------------------------------------------------
+template <int VPL, int MAXT, bool HS, bool NS, bool REPLAY>
+__device__ __forceinline__ void sg_center(const TrainArgs& a, const int32_t* sent, int len, int i,
+                                          int c, int rw, uint32_t s, float alpha,
+                                          const uint32_t*& rp, Counters& cnt, int lane) {
+  const int lo = max(0, i - a.window + rw), hi = min(len, i + a.window + 1 - rw);
+  const int span = hi - lo;
+  float4 x[VPL], g[VPL];
+  load_row<VPL>(a.W, c, a.pitch, a.d4, lane, x);
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) g[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int ctx_l = (lane < span) ? sent[lo + lane] : 0;
+  cnt.centers += 1;
+  cnt.contexts += (unsigned long long)(span - 1);
+  const int nctx = span - 1;
+  const int neg = a.negative;
+  const int G = NS ? max(1, kWave / max(neg, 1)) : 1;
+  int negw_l = 0;
+  int slot = 0;
+  for (int j = lo; j < hi; ++j) {
+    if (j == i) continue;
+    const int w = readlane_i(ctx_l, j - lo);
+    if (HS) hs_word<VPL, MAXT>(a, w, lane, x, g, alpha, cnt);
+    if (NS) {
+      const int gs = slot % G;
+      if (gs == 0) {
+        const int nd = min(G, nctx - slot) * neg;
+        negw_l = draw_negatives<REPLAY>(a, s, (uint32_t)i, slot, nd, lane, rp);
+        cnt.draws += (unsigned long long)nd;
+      }
+      ns_word<VPL, MAXT>(a, a.C, w, negw_l, gs * neg, lane, x, g, alpha, cnt);
+    }
+    ++slot;
+  }
+  float4 cur[VPL];
+  load_row<VPL>(a.W, c, a.pitch, a.d4, lane, cur);
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    cur[v].x += g[v].x;
+    cur[v].y += g[v].y;
+    cur[v].z += g[v].z;
+    cur[v].w += g[v].w;
+  }
+  store_row<VPL>(a.W, c, a.pitch, a.d4, lane, cur);
+}
+
+// ---------------------------------------------------------------------------
+// CBOW center (Word2Vec.cpp:286-315).
+// ---------------------------------------------------------------------------
+template <int VPL, int MAXT, bool HS, bool NS, bool REPLAY>
+__device__ __forceinline__ void cbow_center(const TrainArgs& a, const int32_t* sent, int len,
+                                            int i, int c, int rw, uint32_t s, float alpha,
+                                            const uint32_t*& rp, Counters& cnt, int lane) {
+  const int lo = max(0, i - a.window + rw), hi = min(len, i + a.window + 1 - rw);
+  const int n = hi - lo - 1;  // neu1_num, positional
+  if (n <= 0) return;
+  const int span = hi - lo;
+  const int me = i - lo;
+  const bool valid = lane < span && lane != me;
+  const int id = valid ? sent[lo + lane] : 0;
+  // std::set semantics: unique ids, visited in ascending order.
+  bool dup = !valid;
+  for (int j = 0; j < span; ++j) {
+    const int v = readlane_i(id, j);
+    dup = dup || (j != me && j < lane && v == id);
+  }
+  const unsigned long long uniq = ballot(!dup);
+  const int U = __popcll(uniq);
+  int rank = 0;
+  {
+    unsigned long long m = uniq;
+    while (m) {
+      const int b = __builtin_ctzll(m);
+      m &= m - 1;
+      rank += (readlane_i(id, b) < id) ? 1 : 0;
+    }
+  }
+  int sid = 0;
+  {
+    unsigned long long m = uniq;
+    while (m) {
+      const int b = __builtin_ctzll(m);
+      m &= m - 1;
+      const int v = readlane_i(id, b), rk = readlane_i(rank, b);
+      if (lane == rk) sid = v;
+    }
+  }
+  cnt.centers += 1;
+  cnt.contexts += (unsigned long long)U;
+  float4 h[VPL], g[VPL];
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    h[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+    g[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (int r0 = 0; r0 < U; r0 += MAXT) {
+    float4 rr[MAXT][VPL];
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t)
+      if (r0 + t < U) load_row<VPL>(a.C, readlane_i(sid, r0 + t), a.pitch, a.d4, lane, rr[t]);
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t)
+      if (r0 + t < U) {
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) {
+          h[v].x += rr[t][v].x;
+          h[v].y += rr[t][v].y;
+          h[v].z += rr[t][v].z;
+          h[v].w += rr[t][v].w;
+        }
+      }
+  }
+  const float nf = (float)n;
+  if (a.cbow_mean) {
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      h[v].x /= nf; h[v].y /= nf; h[v].z /= nf; h[v].w /= nf;
+    }
+  }
+  if (HS) hs_word<VPL, MAXT>(a, c, lane, h, g, alpha, cnt);
+  if (NS) {
+    const int nd = a.negative;
+    const int negw_l = draw_negatives<REPLAY>(a, s, (uint32_t)i, 0, nd, lane, rp);
+    cnt.draws += (unsigned long long)nd;
+    ns_word<VPL, MAXT>(a, a.W, c, negw_l, 0, lane, h, g, alpha, cnt);
+  }
+  if (a.cbow_mean) {
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      g[v].x /= nf; g[v].y /= nf; g[v].z /= nf; g[v].w /= nf;
+    }
+  }
+  for (int r0 = 0; r0 < U; r0 += MAXT) {
+    float4 rr[MAXT][VPL];
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t)
+      if (r0 + t < U) load_row<VPL>(a.C, readlane_i(sid, r0 + t), a.pitch, a.d4, lane, rr[t]);
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t)
+      if (r0 + t < U) {
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) {
+          rr[t][v].x += g[v].x;
+          rr[t][v].y += g[v].y;
+          rr[t][v].z += g[v].z;
+          rr[t][v].w += g[v].w;
+        }
+        store_row<VPL>(a.C, readlane_i(sid, r0 + t), a.pitch, a.d4, lane, rr[t]);
+      }
+  }
+}
+
+template <int VPL, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY>
+__device__ __forceinline__ void center(const TrainArgs& a, const int32_t* sent, int len, int i,
+                                       int c, int rw, uint32_t s, float alpha,
+                                       const uint32_t*& rp, Counters& cnt, int lane) {
+  if (CBOW)
+    cbow_center<VPL, MAXT, HS, NS, REPLAY>(a, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
+  else
+    sg_center<VPL, MAXT, HS, NS, REPLAY>(a, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
+}
+
+// ---------------------------------------------------------------------------
+// The epoch kernel: wavefronts dequeue sentences (Word2Vec.cpp:375-394).
+// ---------------------------------------------------------------------------
+template <int VPL, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY>
+__global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
+  const int lane = lane_id();
+  Counters cnt;
+  float alpha = a.init_alpha;
+  bool first = true;
+  const uint32_t wmax = (uint32_t)(a.window < 1 ? 1 : a.window);
+  for (;;) {
+    uint32_t k = 0;
+    if (lane == 0) k = atomicAdd(a.work, 1u);
+    k = (uint32_t)uniform_i((int)k);
+    if ((int64_t)k >= a.n_sent) break;
+    const int64_t s = a.order ? a.order[k] : (int64_t)k;
+    if (first || (k % 10u) == 0u) {
+      const unsigned long long cw =
+          __hip_atomic_load(a.words, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float al =
+          (float)(a.init_alpha * (1.0 - 1.0 / a.iter * (double)cw / a.train_words));
+      alpha = (a.min_alpha < al) ? al : a.min_alpha;
+      first = false;
+    }
+    const int64_t base = a.soff[s];
+    const int len = (int)(a.soff[s + 1] - base);
+    const int32_t* sent = a.ids + base;
+    const uint32_t* rp = nullptr;
+    if (REPLAY) {
+      rp = a.replay + a.replay_off[s];
+      for (int i = 0; i < len; ++i) {
+        const int c = sent[i];
+        const float u = __int_as_float((int)rp[0]);
+        ++rp;
+        if (a.keep[c] < u) continue;
+        const int rw = (int)rp[0];
+        ++rp;
+        center<VPL, MAXT, CBOW, HS, NS, REPLAY>(a, sent, len, i, c, rw, (uint32_t)s, alpha, rp,
+                                                cnt, lane);
+      }
+    } else {
+      for (int i0 = 0; i0 < len; i0 += kWave) {
+        const int ii = i0 + lane;
+        const bool in = ii < len;
+        const int c_l = in ? sent[ii] : 0;
+        const float p_l = in ? a.keep[c_l] : 0.f;
+        uint32_t o0, o1, o2, o3;
+        philox((uint32_t)ii, (uint32_t)s, 0xFFFFFFFFu, a.epoch, a.key0, a.key1, o0, o1, o2, o3);
+        const float u_l = canonical_f(o0);
+        const int rw_l = (int)(((uint64_t)o1 * wmax) >> 32);
+        unsigned long long kept = ballot(in && !(p_l < u_l));
+        while (kept) {
+          const int b = __builtin_ctzll(kept);
+          kept &= kept - 1;
+          const int c = readlane_i(c_l, b), rw = readlane_i(rw_l, b);
+          center<VPL, MAXT, CBOW, HS, NS, REPLAY>(a, sent, len, i0 + b, c, rw, (uint32_t)s,
+                                                  alpha, rp, cnt, lane);
+        }
+      }
+    }
+    if (lane == 0) atomicAdd(a.words, (unsigned long long)len);
+    cnt.sentences += 1;
+  }
+  if (lane == 0) {
+    atomicAdd(&a.stats[0], cnt.centers);
+    atomicAdd(&a.stats[1], cnt.contexts);
+    atomicAdd(&a.stats[2], cnt.targets);
+    atomicAdd(&a.stats[3], cnt.draws);
+    atomicAdd(&a.stats[4], cnt.sentences);
+  }
+}
+
+// Sequential target updates for w2v_dev_apply_targets (one wave).
+template <int VPL>
+__global__ __launch_bounds__(64) void apply_targets_kernel(float* M, int64_t pitch, int d4,
+                                                           const float* x_in, float* grad_io,
+                                                           const int64_t* rows,
+                                                           const uint8_t* codes, int n,
+                                                           float alpha, int hs_form) {
+  const int lane = lane_id();
+  float4 x[VPL], g[VPL];
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int e = 4 * (lane + kWave * v);
+    x[v] = (e < d4) ? *reinterpret_cast<const float4*>(x_in + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    g[v] = (e < d4) ? *reinterpret_cast<const float4*>(grad_io + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (int t = 0; t < n; ++t) {
+    const int row = (int)rows[t];
+    const int code = (int)codes[t];
+    if (hs_form)
+      apply_targets<VPL, 1, true>(M, pitch, d4, lane, 1, row, code, 0, x, g, alpha);
+    else
+      apply_targets<VPL, 1, false>(M, pitch, d4, lane, 1, row, code, 0, x, g, alpha);
+  }
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int e = 4 * (lane + kWave * v);
+    if (e < d4) *reinterpret_cast<float4*>(grad_io + e) = g[v];
+  }
+}
+
+// Expand the monotone unigram table from its V+1 first-index boundaries.
+__global__ void expand_table_kernel(const int64_t* bounds, int64_t V, uint32_t* table, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    int64_t lo = 0, hi = V - 1;  // largest w with bounds[w] <= i
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (bounds[mid] <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    table[i] = (uint32_t)lo;
+  }
+}
+
+}  // namespace w2v

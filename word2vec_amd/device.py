@@ -1,0 +1,177 @@
+"""Python handle over the C-ABI (include/w2v_dev.h): HBM-resident training state.
+
+This is the thin plumbing the tests, the bench and the multi-GPU driver use;
+the C++ host class (include/Word2Vec.h) drives the same C-ABI. All compute runs
+in the HIP kernels of libw2v_hip.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native as N
+
+
+def _ptr(a: np.ndarray | None):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "arrays passed to the C-ABI must be C-contiguous"
+    return a.ctypes.data_as(C.c_void_p)
+
+
+@dataclass
+class Config:
+    """Mirror of w2v_dev_config (Word2Vec ctor fields, Word2Vec.h:64-66)."""
+
+    word_dim: int = 200
+    window: int = 5
+    negative: int = 0
+    hs: bool = True
+    cbow: bool = True
+    cbow_mean: bool = False
+    iter: int = 1
+    init_alpha: float = 0.025
+    min_alpha: float = 1e-6
+    table_size: int = 100_000_000
+    device: int = -1
+
+    def to_c(self) -> N.DevConfig:
+        return N.DevConfig(
+            int(self.word_dim), int(self.window), int(self.negative), int(bool(self.hs)),
+            int(bool(self.cbow)), int(bool(self.cbow_mean)), int(self.iter),
+            float(self.init_alpha), float(self.min_alpha), int(self.table_size),
+            int(self.device), 0,
+        )
+
+
+class DeviceTrainer:
+    """Owns one w2v_dev handle (one GPU)."""
+
+    def __init__(self, cfg: Config):
+        self.lib = N.load_dev_lib()
+        self.cfg = cfg
+        h = C.c_void_p()
+        c = cfg.to_c()
+        N.check(self.lib, self.lib.w2v_dev_create(C.byref(c), C.byref(h)), "w2v_dev_create")
+        self.h = h
+        self.V = 0
+
+    # -- lifecycle -----------------------------------------------------------
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.w2v_dev_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc, what):
+        N.check(self.lib, rc, what)
+
+    # -- configuration -------------------------------------------------------
+    def set_stream(self, stream_handle: int | None):
+        self._chk(self.lib.w2v_dev_set_stream(self.h, C.c_void_p(stream_handle or 0) if stream_handle else None),
+                  "w2v_dev_set_stream")
+
+    def set_rng(self, mode: int, seed: int = 0):
+        self._chk(self.lib.w2v_dev_set_rng(self.h, mode, seed & ((1 << 64) - 1)), "w2v_dev_set_rng")
+
+    def set_schedule(self, sched: int):
+        self._chk(self.lib.w2v_dev_set_schedule(self.h, sched), "w2v_dev_set_schedule")
+
+    # -- uploads -------------------------------------------------------------
+    def upload_vocab(self, sample_prob, table_bounds=None, codes=None, points=None, code_offsets=None):
+        sp = np.ascontiguousarray(sample_prob, dtype=np.float32)
+        tb = None if table_bounds is None else np.ascontiguousarray(table_bounds, dtype=np.int64)
+        cd = None if codes is None else np.ascontiguousarray(codes, dtype=np.uint8)
+        pt = None if points is None else np.ascontiguousarray(points, dtype=np.int32)
+        co = None if code_offsets is None else np.ascontiguousarray(code_offsets, dtype=np.int64)
+        self._chk(self.lib.w2v_dev_upload_vocab(self.h, sp.size, _ptr(sp), _ptr(tb), _ptr(cd), _ptr(pt), _ptr(co)),
+                  "w2v_dev_upload_vocab")
+        self.V = sp.size
+
+    def upload_table(self, table):
+        t = np.ascontiguousarray(table, dtype=np.uint32)
+        self._chk(self.lib.w2v_dev_upload_table(self.h, _ptr(t), t.size), "w2v_dev_upload_table")
+
+    def upload_model(self, W=None, C_=None, S=None):
+        d = self.cfg.word_dim
+        arrs = [None if a is None else np.ascontiguousarray(a, dtype=np.float32).reshape(-1, d) for a in (W, C_, S)]
+        self._chk(self.lib.w2v_dev_upload_model(self.h, *[_ptr(a) for a in arrs]), "w2v_dev_upload_model")
+
+    def download_model(self):
+        d, V = self.cfg.word_dim, self.V
+        W = np.empty((V, d), np.float32)
+        need_c = self.cfg.negative > 0 or self.cfg.cbow
+        Cm = np.empty((V, d), np.float32) if need_c else None
+        S = np.empty((max(V - 1, 0), d), np.float32) if self.cfg.hs else None
+        self._chk(self.lib.w2v_dev_download_model(self.h, _ptr(W), _ptr(Cm), _ptr(S)), "w2v_dev_download_model")
+        return W, Cm, S
+
+    def bind_model(self, dW: int, dC: int | None, dS: int | None, pitch: int):
+        """Train on caller-owned device buffers (e.g. torch tensors) of row pitch `pitch` floats."""
+        self._chk(self.lib.w2v_dev_bind_model(self.h, C.c_void_p(dW), C.c_void_p(dC) if dC else None,
+                                              C.c_void_p(dS) if dS else None, int(pitch)), "w2v_dev_bind_model")
+
+    def model_layout(self):
+        w, c, s, p = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_int64()
+        self._chk(self.lib.w2v_dev_model_layout(self.h, C.byref(w), C.byref(c), C.byref(s), C.byref(p)),
+                  "w2v_dev_model_layout")
+        return w.value, c.value, s.value, p.value
+
+    def upload_corpus(self, ids, sent_offsets, train_words: int):
+        i = np.ascontiguousarray(ids, dtype=np.int32)
+        o = np.ascontiguousarray(sent_offsets, dtype=np.int64)
+        self._chk(self.lib.w2v_dev_upload_corpus(self.h, _ptr(i), i.size, _ptr(o), o.size - 1, int(train_words)),
+                  "w2v_dev_upload_corpus")
+        self.n_sent = o.size - 1
+
+    def upload_replay(self, stream, offsets):
+        s = np.ascontiguousarray(stream, dtype=np.uint32)
+        o = np.ascontiguousarray(offsets, dtype=np.int64)
+        self._chk(self.lib.w2v_dev_upload_replay(self.h, _ptr(s), s.size, _ptr(o), o.size), "w2v_dev_upload_replay")
+
+    # -- training ------------------------------------------------------------
+    def set_progress(self, cw: int):
+        self._chk(self.lib.w2v_dev_set_progress(self.h, int(cw)), "w2v_dev_set_progress")
+
+    def get_progress(self) -> int:
+        v = C.c_int64()
+        self._chk(self.lib.w2v_dev_get_progress(self.h, C.byref(v)), "w2v_dev_get_progress")
+        return v.value
+
+    def train_epoch(self, epoch: int, order=None) -> dict:
+        st = N.DevStats()
+        o = None if order is None else np.ascontiguousarray(order, dtype=np.int64)
+        self._chk(self.lib.w2v_dev_train_epoch(self.h, int(epoch), _ptr(o), C.byref(st)), "w2v_dev_train_epoch")
+        return st.as_dict()
+
+    def train_epoch_async(self, epoch: int, order_dev_ptr: int | None = None):
+        self._chk(self.lib.w2v_dev_train_epoch_async(self.h, int(epoch),
+                                                     C.c_void_p(order_dev_ptr) if order_dev_ptr else None),
+                  "w2v_dev_train_epoch_async")
+
+    def synchronize(self):
+        self._chk(self.lib.w2v_dev_synchronize(self.h), "w2v_dev_synchronize")
+
+    def read_stats(self) -> dict:
+        st = N.DevStats()
+        self._chk(self.lib.w2v_dev_read_stats(self.h, C.byref(st)), "w2v_dev_read_stats")
+        return st.as_dict()
+
+    def reset_stats(self):
+        self._chk(self.lib.w2v_dev_reset_stats(self.h), "w2v_dev_reset_stats")
+
+    def apply_targets(self, which: int, x, grad, rows, codes, alpha: float, hs_form: bool):
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        g = np.array(grad, dtype=np.float32, copy=True)
+        r = np.ascontiguousarray(rows, dtype=np.int64)
+        c = np.ascontiguousarray(codes, dtype=np.uint8)
+        self._chk(self.lib.w2v_dev_apply_targets(self.h, int(which), _ptr(x), _ptr(g), _ptr(r), _ptr(c), r.size,
+                                                 float(alpha), int(bool(hs_form))), "w2v_dev_apply_targets")
+        return g
