@@ -132,7 +132,8 @@ def main():
                  cbow_mean=True, iter=iters_total, init_alpha=0.025 if not mode["cbow"] else 0.05,
                  min_alpha=2.5e-6, table_size=args.table_size, device=local)
     tr = DeviceTrainer(cfg)
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream(device=dev)  # the kernels, the events and RCCL all run on this stream
+    torch.cuda.set_stream(stream)
     tr.set_stream(stream.cuda_stream)
     tr.upload_vocab(keep, bounds, codes, points, coff)
     pitch = (d + 31) // 32 * 32
