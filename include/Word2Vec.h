@@ -1,0 +1,129 @@
+// Word2Vec.h — the reference's class API (/root/reference/Word2Vec.h:29-90),
+// same members, constructor defaults and method signatures, with the training
+// hot path running on an MI355X through the C-ABI in w2v_dev.h.
+//
+// What stays on the host (C++11): vocabulary, Huffman tree, unigram table,
+// subsampling probabilities, weight init, sentence shuffling and the vector
+// files — all bit-identical to the reference. What moves to HBM: W, C and
+// synapses1, the table, the sample probabilities, the Huffman paths and the
+// corpus as token ids; every update of train(), train_sentence_*,
+// negative_sampling and hierarchical_softmax runs in the gfx950 kernels.
+//
+// Additive members (not in the reference) are grouped at the end.
+#ifndef W2V_AMD_WORD2VEC_H
+#define W2V_AMD_WORD2VEC_H
+
+#include <cstdint>
+#include <random>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "Word.h"
+#include "w2v_dense.h"
+#include "w2v_dev.h"
+
+using w2v_dense::IOFormat;
+using w2v_dense::RMatrixXf;
+using w2v_dense::RowVectorXf;
+
+class Word2Vec {
+ public:
+  int iter;
+  int window;
+  int min_count;
+  int table_size;
+  int word_dim;
+  int negative;  // number of negative samples
+  float subsample_threshold;
+  float init_alpha;
+  float min_alpha;
+  int num_threads;  // host threads the reference used; unused by the device path
+
+  bool cbow_mean;
+  bool phrase;
+  std::string train_method;  // "hs" or "ns"
+  std::string model;         // "cbow" or "sg"
+
+  std::vector<Word*> vocab;
+  std::vector<std::string> idx2word;
+  std::unordered_map<std::string, WordP> vocab_hash;
+  std::vector<size_t> table;
+
+  RMatrixXf W, synapses1, C;
+
+  std::random_device rd;
+  std::mt19937 generator;
+  std::uniform_int_distribution<int> distribution_window;
+  std::uniform_int_distribution<int> distribution_table;
+  std::uniform_real_distribution<float> uni_dis;
+
+ public:
+  ~Word2Vec(void);
+
+  Word2Vec(int iter = 1, int window = 5, int min_count = 5, int table_size = 100000000, int word_dim = 200,
+           int negative = 0, float subsample_threshold = 0.001, float init_alpha = 0.025,
+           float min_alpha = 1e-6, bool cbow_mean = false, int num_threads = 1,
+           std::string train_method = "hs", std::string model = "cbow");
+
+  std::vector<std::vector<std::string>> line_docs(std::string file_name);
+  void reduce_vocab();
+  void create_huffman_tree();
+  void make_table();
+  void precalc_sampling();
+  void build_vocab(std::vector<std::vector<std::string>>& sentences);
+  void save_vocab(std::string vocab_filename);
+  void read_vocab(std::string vocab_filename);
+
+  void init_weights(size_t vocab_size);
+
+  std::vector<std::vector<Word*>> build_sample(std::vector<std::vector<std::string>>& data);
+
+  RowVectorXf& hierarchical_softmax(Word* predict_word, RowVectorXf& project_rep, RowVectorXf& project_grad,
+                                    float alpha);
+  RowVectorXf& negative_sampling(Word* predict_word, RowVectorXf& project_rep, RowVectorXf& project_grad,
+                                 RMatrixXf& target_matrix, float alpha);
+  void train_sentence_cbow(std::vector<Word*>& sentence, float alpha);
+  void train_sentence_sg(std::vector<Word*>& sentence, float alpha);
+
+  void train(std::vector<std::vector<std::string>>& sentences);
+
+  void save_word2vec(std::string filename, const RMatrixXf& data, bool binary = false);
+  void load_word2vec(std::string word2vec_filename, bool binary = false);
+
+  // ---- additive (not in the reference) ------------------------------------
+  int gpu_device = 0;        // HIP device ordinal used by the hot path
+  bool replay_rng = false;   // true: the device consumes this object's own mt19937
+                             // stream in the reference's draw order, on one
+                             // wavefront (deterministic, equals the reference run
+                             // single-threaded up to fp32 summation order)
+  bool verbose = true;       // progress line per epoch (the reference prints one
+                             // every 100 sentences, Word2Vec.cpp:382-386)
+  // Train on a corpus that is already token ids (no strings): ids index
+  // `vocab`, sentence s spans [offsets[s], offsets[s+1]); train_words as in
+  // Word2Vec.cpp:362-363 (raw tokens incl. OOV). For corpora too large for
+  // vector<vector<string>>.
+  void train_ids(const std::vector<int32_t>& ids, const std::vector<int64_t>& offsets, int64_t train_words);
+  // Last device error (empty if none).
+  std::string last_error;
+
+ private:
+  w2v_dev* dev_ = nullptr;
+  w2v_dev_config dev_cfg_{};        // configuration dev_ was created with
+  bool dev_vocab_stale_ = true;     // vocab products changed since the last upload
+  int64_t cur_words_ = 0;           // current_words after the last train call
+
+  bool uses_C() const;
+  void ensure_device();
+  void upload_vocab_products();
+  void check(int rc, const char* what);
+  void run_epochs(const std::vector<int32_t>& ids, const std::vector<int64_t>& offsets, int64_t train_words);
+  void append_reference_draws(const std::vector<int32_t>& ids, const std::vector<int64_t>& offsets,
+                              const std::vector<long>& order, std::vector<uint32_t>& stream,
+                              std::vector<int64_t>& stream_off, int64_t epoch);
+  void train_one_sentence(std::vector<Word*>& sentence, float alpha, bool cbow);
+  void apply_rows(RMatrixXf& M, int which, const std::vector<size_t>& rows, const std::vector<uint8_t>& codes,
+                  RowVectorXf& x, RowVectorXf& grad, float alpha, bool hs_form);
+};
+
+#endif  // W2V_AMD_WORD2VEC_H

@@ -140,16 +140,21 @@ int w2v_dev_synchronize(w2v_dev* h);
 int w2v_dev_read_stats(w2v_dev* h, w2v_dev_stats* stats); /* cumulative; synchronizes */
 int w2v_dev_reset_stats(w2v_dev* h);
 
+/* Word2Vec::train_sentence_* take alpha from the caller (Word2Vec.h:83-84):
+ * alpha > 0 makes every following epoch use it instead of the schedule of
+ * Word2Vec.cpp:379-380; alpha <= 0 restores the schedule. */
+int w2v_dev_set_fixed_alpha(w2v_dev* h, float alpha);
+
 /* Replaces: negative_sampling / hierarchical_softmax called on their own
  * (Word2Vec.cpp:232-271, public API Word2Vec.h:81-82). Applies, in order, the
- * n target updates {row rows[t] of matrix `which` (0 = W, 1 = C, 2 =
- * synapses1), code codes[t]} against input `x`, accumulating into `grad`
- * (host arrays of word_dim floats; grad is read and written). hs_form selects
- * the HS arithmetic (g = (1 - code - f) * alpha in double, :241-242) or the NS
- * one (g = (label - f) * alpha with label = 1 - code, :263-264). */
-int w2v_dev_apply_targets(w2v_dev* h, int32_t which, const float* x, float* grad,
-                          const int64_t* rows, const uint8_t* codes, int32_t n, float alpha,
-                          int32_t hs_form);
+ * n target updates to `rows` (host, n dense rows of word_dim floats, read and
+ * written; the rows must be distinct — they are the unique NS targets or the
+ * nodes of one Huffman path) with codes[t] (HS: Huffman code; NS: 1 - label),
+ * input `x` and gradient accumulator `grad` (host, word_dim floats, read and
+ * written). hs_form selects the HS arithmetic (g = (1 - code - f) * alpha in
+ * double, :241-242) or the NS one (g = (label - f) * alpha, :263-264). */
+int w2v_dev_apply_rows(w2v_dev* h, float* rows, const uint8_t* codes, int32_t n, const float* x,
+                       float* grad, float alpha, int32_t hs_form);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,63 @@
+/*
+ * w2v_model.h — a C bridge over the C++ Word2Vec class (include/Word2Vec.h),
+ * for FFI callers (Python ctypes in tests/, cgo/JNI-style bindings). Each call
+ * maps onto one class member of the reference API (Word2Vec.h:61-90); no
+ * exception crosses it: failures return non-zero and set w2v_model_last_error.
+ * which: 0 = W, 1 = C, 2 = synapses1.
+ */
+#ifndef W2V_MODEL_H
+#define W2V_MODEL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct w2v_model w2v_model;
+
+/* Word2Vec(iter, window, min_count, table_size, word_dim, negative, subsample_threshold,
+ *          init_alpha, min_alpha, cbow_mean, num_threads, train_method, model) */
+w2v_model* w2v_model_new(int32_t iter, int32_t window, int32_t min_count, int32_t table_size, int32_t word_dim,
+                         int32_t negative, float subsample_threshold, float init_alpha, float min_alpha,
+                         int32_t cbow_mean, int32_t num_threads, const char* train_method, const char* model);
+void w2v_model_free(w2v_model* m);
+const char* w2v_model_last_error(w2v_model* m);
+void w2v_model_seed(w2v_model* m, uint32_t seed);               /* generator.seed(seed) */
+void w2v_model_options(w2v_model* m, int32_t gpu_device, int32_t replay_rng, int32_t verbose);
+
+/* Sentences as text: one per line, whitespace-separated tokens (line_docs format). */
+int w2v_model_build_vocab(w2v_model* m, const char* text, int64_t len);
+int w2v_model_train(w2v_model* m, const char* text, int64_t len);
+int w2v_model_train_ids(w2v_model* m, const int32_t* ids, const int64_t* offsets, int64_t n_sent,
+                        int64_t train_words);
+int w2v_model_init_weights(w2v_model* m);
+
+int64_t w2v_model_vocab_size(w2v_model* m);
+const char* w2v_model_word(w2v_model* m, int64_t i);
+int64_t w2v_model_word_count(w2v_model* m, int64_t i);
+float w2v_model_sample_probability(w2v_model* m, int64_t i);
+int64_t w2v_model_path_length(w2v_model* m, int64_t i);
+int w2v_model_path(w2v_model* m, int64_t i, uint8_t* codes, int32_t* points);
+int64_t w2v_model_table_length(w2v_model* m);
+int w2v_model_table(w2v_model* m, uint32_t* out);
+
+int64_t w2v_model_rows(w2v_model* m, int32_t which);
+int w2v_model_get_matrix(w2v_model* m, int32_t which, float* out);
+int w2v_model_set_matrix(w2v_model* m, int32_t which, const float* in, int64_t rows);
+
+/* train_sentence_sg / train_sentence_cbow on one sentence of vocab indices. */
+int w2v_model_train_sentence(w2v_model* m, const int32_t* ids, int64_t n, float alpha, int32_t cbow);
+/* negative_sampling (which = 0 or 1) / hierarchical_softmax for word `word`. */
+int w2v_model_negative_sampling(w2v_model* m, int64_t word, float* x, float* grad, int32_t which, float alpha);
+int w2v_model_hierarchical_softmax(w2v_model* m, int64_t word, float* x, float* grad, float alpha);
+
+int w2v_model_save(w2v_model* m, const char* path, int32_t which, int32_t binary);
+int w2v_model_load(w2v_model* m, const char* path, int32_t binary);
+int w2v_model_save_vocab(w2v_model* m, const char* path);
+int w2v_model_read_vocab(w2v_model* m, const char* path);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* W2V_MODEL_H */

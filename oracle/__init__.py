@@ -58,6 +58,9 @@ _SIG = {
     "orc_train_omp": (_I64, [_P, _I32, _I64, _U32]),
     "orc_set_vocab_counts": (None, [_P, _P, _I64]),
     "orc_set_samples": (None, [_P, _P, _P, _I64, _I64]),
+    "orc_train_sentence": (None, [_P, _P, _I64, _F, _I32]),
+    "orc_negative_sampling": (None, [_P, _I64, _P, _P, _I32, _F]),
+    "orc_hierarchical_softmax": (None, [_P, _I64, _P, _P, _F]),
 }
 
 _lib = None
@@ -211,6 +214,22 @@ class Oracle:
         ids = np.ascontiguousarray(ids, np.int32)
         off = np.ascontiguousarray(off, np.int64)
         self.L.orc_set_samples(self.h, _p(ids), _p(off), off.size - 1, int(train_words))
+
+    def train_sentence(self, ids, alpha: float, cbow: bool):
+        ids = np.ascontiguousarray(ids, np.int32)
+        self.L.orc_train_sentence(self.h, _p(ids), ids.size, alpha, int(cbow))
+
+    def negative_sampling(self, word, x, grad, which, alpha):
+        x = np.ascontiguousarray(x, np.float32)
+        g = np.array(grad, np.float32)
+        self.L.orc_negative_sampling(self.h, word, _p(x), _p(g), which, alpha)
+        return g
+
+    def hierarchical_softmax(self, word, x, grad, alpha):
+        x = np.ascontiguousarray(x, np.float32)
+        g = np.array(grad, np.float32)
+        self.L.orc_hierarchical_softmax(self.h, word, _p(x), _p(g), alpha)
+        return g
 
 
 def philox(ctr, key: int):

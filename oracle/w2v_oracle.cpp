@@ -700,4 +700,20 @@ void orc_set_samples(void* h, const int32_t* ids, const int64_t* off, int64_t n_
   m.train_words = train_words;
 }
 
+// The public per-call methods (Word2Vec.h:81-84) on the oracle's generator.
+void orc_train_sentence(void* h, const int32_t* ids, int64_t n, float alpha, int32_t cbow) {
+  Orc& m = *H(h);
+  RefDraws dr(&m.gen, m.cfg.window, m.cfg.table_size, nullptr);
+  if (cbow) cbow_sentence(m, ids, (int)n, alpha, dr, 0);
+  else sg_sentence(m, ids, (int)n, alpha, dr, 0);
+}
+void orc_negative_sampling(void* h, int64_t word, const float* x, float* grad, int32_t which, float alpha) {
+  Orc& m = *H(h);
+  RefDraws dr(&m.gen, m.cfg.window, m.cfg.table_size, nullptr);
+  ns_step(m, (int)word, x, grad, which == 0 ? m.W.data() : m.C.data(), alpha, dr, 0);
+}
+void orc_hierarchical_softmax(void* h, int64_t word, const float* x, float* grad, float alpha) {
+  hs_step(*H(h), (int)word, x, grad, alpha);
+}
+
 }  // extern "C"

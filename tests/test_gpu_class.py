@@ -1,0 +1,115 @@
+"""The C++ Word2Vec class end to end on the GPU against the oracle: train()
+in replay mode (the reference's own mt19937 draws), the per-call methods
+train_sentence_*, negative_sampling, hierarchical_softmax, and the CLI."""
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from tests.corpus import zipf_sentences
+from tests.harness import MODES, oracle_run, rel_err
+from word2vec_amd.model import Word2Vec
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _pair(mode, sents, dim=32, iters=2, seed=5, replay=True, ts=50_000):
+    m = MODES[mode]
+    w = Word2Vec(iter=iters, window=5, min_count=2, table_size=ts, word_dim=dim, negative=m["negative"],
+                 subsample_threshold=1e-3, init_alpha=0.05, min_alpha=2.5e-6, cbow_mean=True,
+                 train_method=m["train_method"], model=m["model"], replay_rng=replay)
+    w.seed(seed)
+    w.build_vocab(sents)
+    w.init_weights()
+    return w
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+def test_class_train_replay_matches_oracle(mode):
+    sents = zipf_sentences(10, 150, 300, seed=12, ragged=True)
+    w = _pair(mode, sents)
+    w.train(sents)
+    o = oracle_run(sents, mode, dim=32, iters=2, table_size=50_000, seed=5)
+    for k in range(3):
+        want, init = o.matrix(k), o.matrix(k, True)
+        if want.size == 0:
+            continue
+        got = w.matrix(k)
+        assert got.shape == want.shape
+        assert rel_err(got - init, want - init) < 1e-4, (mode, k)
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+def test_class_train_sentence_matches_oracle(mode):
+    sents = zipf_sentences(6, 120, 200, seed=13)
+    w = _pair(mode, sents, iters=1)
+    o = oracle_run(sents, mode, dim=32, iters=1, table_size=50_000, seed=5, train=False)
+    o.build_sample()
+    ids, off = o.samples()
+    cbow = MODES[mode]["model"] == "cbow"
+    init = [o.matrix(k) for k in range(3)]
+    for s in range(3):
+        sent = ids[off[s]:off[s + 1]]
+        w.train_sentence(sent, 0.03, cbow)
+        o.train_sentence(sent, 0.03, cbow)
+    for k in range(3):
+        want = o.matrix(k)
+        if want.size == 0:
+            continue
+        assert rel_err(w.matrix(k) - init[k], want - init[k]) < 1e-5, (mode, k)
+
+
+def test_class_negative_sampling_and_hs_match_oracle():
+    sents = zipf_sentences(6, 200, 150, seed=14)
+    for mode in ("sg_ns", "sg_hs"):
+        w = _pair(mode, sents, iters=1)
+        o = oracle_run(sents, mode, dim=32, iters=1, table_size=50_000, seed=5, train=False)
+        rng = np.random.default_rng(1)
+        # give the output matrices content so the updates are non-trivial
+        k_out = 1 if mode == "sg_ns" else 2
+        M = rng.standard_normal(o.matrix(k_out).shape).astype(np.float32) * 0.1
+        w.set_matrix(k_out, M)
+        o.set_matrix(k_out, M)
+        for word in (0, 3, 17):
+            x = rng.standard_normal(32).astype(np.float32) * 0.1
+            g0 = rng.standard_normal(32).astype(np.float32) * 0.01
+            if mode == "sg_ns":
+                gw = w.negative_sampling(word, x, g0, 1, 0.025)
+                go = o.negative_sampling(word, x, g0, 1, 0.025)
+            else:
+                gw = w.hierarchical_softmax(word, x, g0, 0.025)
+                go = o.hierarchical_softmax(word, x, g0, 0.025)
+            assert rel_err(gw - g0, go - g0) < 1e-5
+        assert rel_err(w.matrix(k_out) - M, o.matrix(k_out) - M) < 1e-5
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+def test_class_train_parallel_philox(mode):
+    sents = zipf_sentences(300, 500, 3000, seed=15, ragged=True)
+    w = _pair(mode, sents, dim=100, replay=False, ts=1_000_000)
+    before = [w.matrix(k).copy() for k in range(3)]
+    w.train(sents)
+    for k in range(3):
+        m = w.matrix(k)
+        assert np.isfinite(m).all()
+    moved = [np.abs(w.matrix(k) - before[k]).max() for k in range(3) if before[k].size]
+    assert max(moved) > 0
+
+
+def test_cli_end_to_end(tmp_path):
+    sents = zipf_sentences(50, 1000, 2000, seed=16)
+    corpus = tmp_path / "corpus.txt"
+    corpus.write_text(" ".join(" ".join(s) for s in sents))
+    out = tmp_path / "vec.txt"
+    vocab = tmp_path / "vocab.txt"
+    r = subprocess.run([str(ROOT / "word2vec_amd" / "bin" / "word2vec"), "-train", str(corpus), "-output", str(out),
+                        "-size", "64", "-negative", "5", "-iter", "2", "-save-vocab", str(vocab)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = out.read_text().splitlines()
+    V, d = map(int, lines[0].split())
+    assert d == 64 and len(lines) == V + 1 == len(vocab.read_text().splitlines()) + 1
+    vals = np.array([float(x) for x in lines[1].split()[1:]])
+    assert vals.size == 64 and np.isfinite(vals).all()

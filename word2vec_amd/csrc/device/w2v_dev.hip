@@ -64,10 +64,10 @@ struct w2v_dev {
   int64_t n_replay_off = 0;
   unsigned long long* counters = nullptr;  // [0] words, [1..5] stats
   unsigned int* work = nullptr;
-  float* scratch_f = nullptr;      // x | grad for apply_targets
-  int64_t* scratch_rows = nullptr;
+  float* scratch_f = nullptr;      // x | grad | rows for apply_rows
   uint8_t* scratch_codes = nullptr;
-  int64_t scratch_n = 0;
+  int64_t scratch_n = 0;           // floats in scratch_f
+  float fixed_alpha = 0.0f;
   int32_t rng = W2V_RNG_PHILOX;
   uint64_t seed = 0;
   int32_t sched = W2V_SCHED_PARALLEL;
@@ -176,7 +176,7 @@ void w2v_dev_destroy(w2v_dev* h) {
   dfree(h->keep); dfree(h->table); dfree(h->codes); dfree(h->points); dfree(h->coff);
   dfree(h->ids); dfree(h->soff); dfree(h->order); dfree(h->replay); dfree(h->replay_off);
   dfree(h->counters); dfree(h->work);
-  dfree(h->scratch_f); dfree(h->scratch_rows); dfree(h->scratch_codes);
+  dfree(h->scratch_f); dfree(h->scratch_codes);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -453,6 +453,7 @@ int w2v_dev_train_epoch_async(w2v_dev* h, int32_t epoch, const int64_t* order_de
   a.stats = h->counters + 1;
   a.key0 = (uint32_t)h->seed; a.key1 = (uint32_t)(h->seed >> 32);
   a.epoch = (uint32_t)epoch;
+  a.fixed_alpha = h->fixed_alpha;
   KernelFn fn = kernel_for(h);
   HIP_TRY(hipMemsetAsync(h->work, 0, sizeof(unsigned int), h->stream));
   dim3 grid(1), block(64);
@@ -532,47 +533,48 @@ int w2v_dev_reset_stats(w2v_dev* h) {
   return W2V_OK;
 }
 
-int w2v_dev_apply_targets(w2v_dev* h, int32_t which, const float* x, float* grad,
-                          const int64_t* rows, const uint8_t* codes, int32_t n, float alpha,
-                          int32_t hs_form) {
+int w2v_dev_set_fixed_alpha(w2v_dev* h, float alpha) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  h->fixed_alpha = alpha > 0 ? alpha : 0.0f;
+  return W2V_OK;
+}
+
+int w2v_dev_apply_rows(w2v_dev* h, float* rows, const uint8_t* codes, int32_t n, const float* x, float* grad,
+                       float alpha, int32_t hs_form) {
   if (!h || !x || !grad || (n > 0 && (!rows || !codes))) return fail(W2V_ERR_ARG, "null argument");
   if (n < 0) return fail(W2V_ERR_ARG, "n < 0");
-  if (!h->model_ready) return fail(W2V_ERR_STATE, "upload the model first");
-  float* M = which == 0 ? h->W : which == 1 ? h->C : which == 2 ? h->S : nullptr;
-  if (!M) return fail(W2V_ERR_ARG, "matrix not resident for this configuration");
-  const int64_t rows_max = which == 2 ? h->V - 1 : h->V;
-  for (int32_t t = 0; t < n; ++t)
-    if (rows[t] < 0 || rows[t] >= rows_max) return fail(W2V_ERR_ARG, "row out of range");
   if (set_device(h)) return W2V_ERR_HIP;
-  if (h->scratch_n < n || !h->scratch_f) {
-    dfree(h->scratch_f); dfree(h->scratch_rows); dfree(h->scratch_codes);
-    const int64_t cap = n > 64 ? n : 64;
-    HIP_TRY(hipMalloc(&h->scratch_f, 2 * (size_t)h->pitch * sizeof(float)));
-    HIP_TRY(hipMalloc(&h->scratch_rows, cap * sizeof(int64_t)));
-    HIP_TRY(hipMalloc(&h->scratch_codes, cap));
-    h->scratch_n = cap;
+  const int64_t need = (int64_t)(n + 2) * h->pitch;
+  if (h->scratch_n < need) {
+    dfree(h->scratch_f); dfree(h->scratch_codes);
+    HIP_TRY(hipMalloc(&h->scratch_f, need * sizeof(float)));
+    HIP_TRY(hipMalloc(&h->scratch_codes, (size_t)(n > 64 ? n : 64)));
+    h->scratch_n = need;
   }
-  const size_t d = (size_t)h->cfg.word_dim;
+  const size_t d = (size_t)h->cfg.word_dim, dp = (size_t)h->pitch * sizeof(float);
   float* dx = h->scratch_f;
   float* dg = h->scratch_f + h->pitch;
-  HIP_TRY(hipMemsetAsync(h->scratch_f, 0, 2 * (size_t)h->pitch * sizeof(float), h->stream));
+  float* dr = h->scratch_f + 2 * h->pitch;
+  HIP_TRY(hipMemsetAsync(h->scratch_f, 0, need * sizeof(float), h->stream));
   HIP_TRY(hipMemcpyAsync(dx, x, d * sizeof(float), hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipMemcpyAsync(dg, grad, d * sizeof(float), hipMemcpyHostToDevice, h->stream));
   if (n > 0) {
-    HIP_TRY(hipMemcpyAsync(h->scratch_rows, rows, n * sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipMemcpy2DAsync(dr, dp, rows, d * sizeof(float), d * sizeof(float), n, hipMemcpyHostToDevice, h->stream));
     HIP_TRY(hipMemcpyAsync(h->scratch_codes, codes, n, hipMemcpyHostToDevice, h->stream));
   }
-  void (*fn)(float*, int64_t, int, const float*, float*, const int64_t*, const uint8_t*, int, float, int);
+  void (*fn)(float*, int64_t, int, const float*, float*, const uint8_t*, int, float, int);
   switch (h->vpl) {
-    case 1: fn = &w2v::apply_targets_kernel<1>; break;
-    case 2: fn = &w2v::apply_targets_kernel<2>; break;
-    case 3: fn = &w2v::apply_targets_kernel<3>; break;
-    default: fn = &w2v::apply_targets_kernel<4>; break;
+    case 1: fn = &w2v::apply_rows_kernel<1>; break;
+    case 2: fn = &w2v::apply_rows_kernel<2>; break;
+    case 3: fn = &w2v::apply_rows_kernel<3>; break;
+    default: fn = &w2v::apply_rows_kernel<4>; break;
   }
-  hipLaunchKernelGGL(fn, dim3(1), dim3(64), 0, h->stream, M, h->pitch, h->d4, dx, dg,
-                     h->scratch_rows, h->scratch_codes, n, alpha, hs_form);
+  hipLaunchKernelGGL(fn, dim3(1), dim3(64), 0, h->stream, dr, h->pitch, h->d4, dx, dg, h->scratch_codes, n,
+                     alpha, hs_form);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(grad, dg, d * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+  if (n > 0)
+    HIP_TRY(hipMemcpy2DAsync(rows, d * sizeof(float), dr, dp, d * sizeof(float), n, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
   return W2V_OK;
 }

@@ -68,6 +68,7 @@ struct TrainArgs {
   unsigned int* work;          // dequeue head
   unsigned long long* stats;   // centers, contexts, targets, draws, sentences
   uint32_t key0, key1, epoch;
+  float fixed_alpha;           // > 0: use instead of the schedule
 };
 
 struct Counters {
@@ -475,7 +476,9 @@ __global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
     k = (uint32_t)uniform_i((int)k);
     if ((int64_t)k >= a.n_sent) break;
     const int64_t s = a.order ? a.order[k] : (int64_t)k;
-    if (first || (k % 10u) == 0u) {
+    if (a.fixed_alpha > 0.0f) {
+      alpha = a.fixed_alpha;
+    } else if (first || (k % 10u) == 0u) {
       const unsigned long long cw =
           __hip_atomic_load(a.words, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const float al =
@@ -531,13 +534,12 @@ __global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
   }
 }
 
-// Sequential target updates for w2v_dev_apply_targets (one wave).
+// Sequential target updates for w2v_dev_apply_rows (one wave): target t is
+// row t of M, applied in order (rows are distinct).
 template <int VPL>
-__global__ __launch_bounds__(64) void apply_targets_kernel(float* M, int64_t pitch, int d4,
-                                                           const float* x_in, float* grad_io,
-                                                           const int64_t* rows,
-                                                           const uint8_t* codes, int n,
-                                                           float alpha, int hs_form) {
+__global__ __launch_bounds__(64) void apply_rows_kernel(float* M, int64_t pitch, int d4, const float* x_in,
+                                                        float* grad_io, const uint8_t* codes, int n, float alpha,
+                                                        int hs_form) {
   const int lane = lane_id();
   float4 x[VPL], g[VPL];
 #pragma unroll
@@ -547,12 +549,11 @@ __global__ __launch_bounds__(64) void apply_targets_kernel(float* M, int64_t pit
     g[v] = (e < d4) ? *reinterpret_cast<const float4*>(grad_io + e) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   for (int t = 0; t < n; ++t) {
-    const int row = (int)rows[t];
     const int code = (int)codes[t];
     if (hs_form)
-      apply_targets<VPL, 1, true>(M, pitch, d4, lane, 1, row, code, 0, x, g, alpha);
+      apply_targets<VPL, 1, true>(M, pitch, d4, lane, 1, t, code, 0, x, g, alpha);
     else
-      apply_targets<VPL, 1, false>(M, pitch, d4, lane, 1, row, code, 0, x, g, alpha);
+      apply_targets<VPL, 1, false>(M, pitch, d4, lane, 1, t, code, 0, x, g, alpha);
   }
 #pragma unroll
   for (int v = 0; v < VPL; ++v) {

@@ -1,0 +1,149 @@
+// word2vec — command-line driver with the reference CLI's flags, defaults and
+// validation (/root/reference/main.cpp:94-204), training on an MI355X.
+//
+// Kept as in the reference: the defaults of main.cpp:105-121 (not those of the
+// help text), the hs/ns validation (:164-178), init_alpha forced to 0.05
+// because cbow_mean is hard-wired true (:117,180-181), min_alpha derived from
+// the pre-override 0.025 (:116), 1000-token sentences (:66), and which matrix
+// is written (:196-201). Additive: -train is honoured (the reference always
+// reads ./text8), -binary, -gpu, -replay.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "Word2Vec.h"
+
+namespace {
+
+void usage() {
+  std::cout << "word2vec (MI355X) — skip-gram / CBOW with negative sampling or hierarchical softmax\n\n"
+               "  -train <file>         training text (default: ./text8)\n"
+               "  -output <file>        word vectors to write (default: text8-sgns.txt)\n"
+               "  -size <int>           vector dimension (default 200)\n"
+               "  -window <int>         max context distance (default 5)\n"
+               "  -subsample <float>    frequent-word down-sampling threshold (default 1e-4)\n"
+               "  -train_method <hs|ns> hierarchical softmax or negative sampling (default ns)\n"
+               "  -negative <int>       negatives per target (default 0; required > 0 for ns)\n"
+               "  -threads <int>        host threads (kept for compatibility; default 1)\n"
+               "  -iter <int>           epochs (default 1)\n"
+               "  -min-count <int>      drop words rarer than this (default 5)\n"
+               "  -alpha <float>        accepted, but the start rate is 0.05 (cbow_mean is always on)\n"
+               "  -save-vocab <file>    write the vocabulary\n"
+               "  -read-vocab <file>    accepted, unused (as in the reference CLI)\n"
+               "  -model <cbow|sg>      architecture (default sg)\n"
+               "  -binary <0|1>         write vectors in the binary layout (default 0)\n"
+               "  -gpu <int>            HIP device (default 0)\n"
+               "  -replay <0|1>         reference-exact deterministic RNG replay on one wavefront\n\n"
+               "example: ./word2vec -train text8 -output vec.txt -size 300 -window 5 -subsample 1e-4 "
+               "-negative 5 -model sg -train_method ns -iter 3\n";
+}
+
+int find_flag(const char* name, int argc, char** argv) {
+  for (int i = 1; i < argc; ++i)
+    if (!std::strcmp(name, argv[i])) {
+      if (i == argc - 1) {
+        std::printf("Argument missing for %s\n", name);
+        std::exit(1);
+      }
+      return i;
+    }
+  return -1;
+}
+
+// main.cpp:63-92: whitespace tokens grouped into 1000-token sentences.
+std::vector<std::vector<std::string>> read_corpus(const std::string& path) {
+  const size_t kSentence = 1000;
+  std::vector<std::vector<std::string>> out;
+  std::ifstream in(path);
+  std::vector<std::string> cur;
+  std::string tok;
+  while (in >> tok) {
+    cur.push_back(tok);
+    if (cur.size() == kSentence) {
+      out.push_back(cur);
+      cur.clear();
+    }
+  }
+  if (!cur.empty()) out.push_back(cur);
+  return out;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc == 1) {
+    usage();
+    return 0;
+  }
+  std::string input_file = "", output_file = "text8-sgns.txt", save_vocab_file = "", read_vocab_file = "";
+  std::string model = "sg", train_method = "ns";
+  int table_size = 100000000, word_dim = 200, window = 5, negative = 0, num_threads = 1, iter = 1, min_count = 5;
+  float init_alpha = 0.025f, subsample_threshold = 0.0001f;
+  const float min_alpha = init_alpha * 0.0001;
+  const bool cbow_mean = true;
+  int binary = 0, gpu = 0, replay = 0;
+  int i;
+  if ((i = find_flag("-size", argc, argv)) > 0) word_dim = std::atoi(argv[i + 1]);
+  if ((i = find_flag("-train", argc, argv)) > 0) input_file = argv[i + 1];
+  if ((i = find_flag("-save-vocab", argc, argv)) > 0) save_vocab_file = argv[i + 1];
+  if ((i = find_flag("-read-vocab", argc, argv)) > 0) read_vocab_file = argv[i + 1];
+  if ((i = find_flag("-model", argc, argv)) > 0) model = argv[i + 1];
+  if ((i = find_flag("-alpha", argc, argv)) > 0) init_alpha = (float)std::atof(argv[i + 1]);
+  if ((i = find_flag("-output", argc, argv)) > 0) output_file = argv[i + 1];
+  if ((i = find_flag("-window", argc, argv)) > 0) window = std::atoi(argv[i + 1]);
+  if ((i = find_flag("-subsample", argc, argv)) > 0) subsample_threshold = (float)std::atof(argv[i + 1]);
+  if ((i = find_flag("-train_method", argc, argv)) > 0) train_method = argv[i + 1];
+  if ((i = find_flag("-negative", argc, argv)) > 0) negative = std::atoi(argv[i + 1]);
+  if ((i = find_flag("-threads", argc, argv)) > 0) num_threads = std::atoi(argv[i + 1]);
+  if ((i = find_flag("-iter", argc, argv)) > 0) iter = std::atoi(argv[i + 1]);
+  if ((i = find_flag("-min-count", argc, argv)) > 0) min_count = std::atoi(argv[i + 1]);
+  if ((i = find_flag("-binary", argc, argv)) > 0) binary = std::atoi(argv[i + 1]);
+  if ((i = find_flag("-gpu", argc, argv)) > 0) gpu = std::atoi(argv[i + 1]);
+  if ((i = find_flag("-replay", argc, argv)) > 0) replay = std::atoi(argv[i + 1]);
+
+  if (model.empty()) {
+    model = "sg";
+    std::cout << "Default use skip gram model" << std::endl;
+  }
+  if (train_method.empty()) {
+    train_method = "ns";
+    std::cout << "Default use negative sampling model" << std::endl;
+  }
+  if (train_method == "ns" && negative <= 0) {
+    std::cout << "Please set -negative > 0!" << std::endl;
+    return 1;
+  }
+  if (train_method == "hs" && negative > 0) {
+    std::cout << "Do not set -negative under hierarchical softmax!" << std::endl;
+    return 1;
+  }
+  if (train_method == "hs" && model.find("align") != std::string::npos) {
+    std::cout << "Please use negative sampling in aligned skip gram model!" << std::endl;
+    return 1;
+  }
+  if (cbow_mean) init_alpha = 0.05f;
+
+  Word2Vec w2v(iter, window, min_count, table_size, word_dim, negative, subsample_threshold, init_alpha,
+               min_alpha, cbow_mean, num_threads, train_method, model);
+  w2v.gpu_device = gpu;
+  w2v.replay_rng = replay != 0;
+  std::vector<std::vector<std::string>> sentences = read_corpus(input_file.empty() ? "text8" : input_file);
+  w2v.build_vocab(sentences);
+  w2v.init_weights(w2v.vocab.size());
+  if (!save_vocab_file.empty()) w2v.save_vocab(save_vocab_file);
+  try {
+    w2v.train(sentences);
+  } catch (const std::exception& e) {
+    std::cerr << e.what() << std::endl;
+    return 2;
+  }
+  if (!output_file.empty()) {
+    if (train_method == "hs" && model == "cbow") w2v.save_word2vec(output_file, w2v.C, binary != 0);
+    else w2v.save_word2vec(output_file, w2v.W, binary != 0);
+  }
+  return 0;
+}

@@ -167,11 +167,15 @@ class DeviceTrainer:
     def reset_stats(self):
         self._chk(self.lib.w2v_dev_reset_stats(self.h), "w2v_dev_reset_stats")
 
-    def apply_targets(self, which: int, x, grad, rows, codes, alpha: float, hs_form: bool):
+    def set_fixed_alpha(self, alpha: float):
+        self._chk(self.lib.w2v_dev_set_fixed_alpha(self.h, float(alpha)), "w2v_dev_set_fixed_alpha")
+
+    def apply_rows(self, rows, codes, x, grad, alpha: float, hs_form: bool):
+        """Sequential NS/HS updates of distinct host rows on the device; returns (rows, grad)."""
+        r = np.array(rows, dtype=np.float32, copy=True).reshape(-1, self.cfg.word_dim)
+        c = np.ascontiguousarray(codes, dtype=np.uint8)
         x = np.ascontiguousarray(x, dtype=np.float32)
         g = np.array(grad, dtype=np.float32, copy=True)
-        r = np.ascontiguousarray(rows, dtype=np.int64)
-        c = np.ascontiguousarray(codes, dtype=np.uint8)
-        self._chk(self.lib.w2v_dev_apply_targets(self.h, int(which), _ptr(x), _ptr(g), _ptr(r), _ptr(c), r.size,
-                                                 float(alpha), int(bool(hs_form))), "w2v_dev_apply_targets")
-        return g
+        self._chk(self.lib.w2v_dev_apply_rows(self.h, _ptr(r), _ptr(c), c.size, _ptr(x), _ptr(g), float(alpha),
+                                              int(bool(hs_form))), "w2v_dev_apply_rows")
+        return r, g
