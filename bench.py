@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--table-size", type=int, default=100_000_000)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--sync-every", type=int, default=0,
+                    help="average the replicas every this many sentences of a shard (0 = once per step)")
     return ap.parse_args()
 
 
@@ -69,14 +71,23 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # W2V_BENCH_SHARE_GPU=1 rehearses the N>1 path on a one-GPU box: every rank
+    # on cuda:0, gloo instead of RCCL (numbers from such a run are not bench lines)
+    share = os.environ.get("W2V_BENCH_SHARE_GPU") == "1"
+    if share:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from word2vec_amd import _native as N
     from word2vec_amd import host
     from word2vec_amd.device import Config, DeviceTrainer
+    from word2vec_amd.replicas import ReplicaGroup, n_rounds, train_rounds
 
     mode = MODES[args.mode]
     neg = 0 if mode["hs"] else args.negative
@@ -147,7 +158,7 @@ def main():
     S = torch.zeros(max(V - 1, 1), pitch, dtype=torch.float32, device=dev) if mode["hs"] else None
     tr.bind_model(W.data_ptr(), Cm.data_ptr() if Cm is not None else None,
                   S.data_ptr() if S is not None else None, pitch)
-    tr.upload_corpus(ids_h, soff_h, n_tok)
+    tr.upload_corpus(ids_h, soff_h, n_tok * world)  # alpha follows the global raw-token total
     tr.set_rng(N.W2V_RNG_PHILOX, (args.seed << 32) | (rank + 1))
     tr.set_schedule(N.W2V_SCHED_PARALLEL)
     tr.set_progress(0)
@@ -155,29 +166,26 @@ def main():
     log(f"[bench] resident in HBM ({time.time() - t0:.1f}s)")
 
     mats = [m for m in (W, Cm, S) if m is not None]
+    replicas = ReplicaGroup(mats, world)
+    rounds = n_rounds(n_sent * world, world, args.sync_every)
+    order_dev = torch.arange(n_sent, dtype=torch.int64, device=dev)  # this rank's shard, in order
+    progress = 0
 
     def step(epoch, evs=None):
-        if evs is not None:
-            evs[0].record(stream)
-        tr.train_epoch_async(epoch)
-        if evs is not None:
-            evs[1].record(stream)
-        if world > 1:
-            for m in mats:  # periodic model averaging over xGMI (RCCL)
-                dist.all_reduce(m, op=dist.ReduceOp.AVG)
+        nonlocal progress
+        progress = train_rounds(tr, replicas, order_dev, epoch, rounds, dev, progress, evs)
 
     for w in range(args.warmup):
         step(w)
     torch.cuda.synchronize()
     st0 = tr.read_stats()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
+    events = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for k in range(args.steps):
-        step(args.warmup + k, events[k])
+        step(args.warmup + k, events)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -185,15 +193,19 @@ def main():
     st1 = tr.read_stats()
     kern_ms = [a.elapsed_time(b) for a, b in events]
     delta = {k: st1[k] - st0[k] for k in st1}
+    # every step trains this rank's whole shard once (the device word counter is
+    # moved to the global count at each averaging round, so count from the shard)
+    assert delta["sentences"] == n_sent * args.steps, delta
+    words_local = int(ids_h.size) * args.steps
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        wsum = torch.tensor([delta["words"]], dtype=torch.int64, device=dev)
+        wsum = torch.tensor([words_local], dtype=torch.int64, device=dev)
         dist.all_reduce(wsum)
         words_total = int(wsum.item())
     else:
-        words_total = delta["words"]
+        words_total = words_local
     for m in mats:
         assert torch.isfinite(m).all().item(), "non-finite weights"
 
@@ -203,7 +215,8 @@ def main():
         row_moves = 2 * delta["contexts"] + 2 * delta["targets"]
     else:
         row_moves = 2 * delta["centers"] + 2 * delta["targets"]
-    bytes_per_launch = (4 * d * row_moves + 4 * delta["draws"]) / args.steps
+    n_launch = max(1, len(events))
+    bytes_per_launch = (4 * d * row_moves + 4 * delta["draws"]) / n_launch
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
     achieved = bytes_per_launch / avg_kernel_s / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -237,7 +250,8 @@ def main():
                 "in_vocab_tokens_per_gpu_per_step": int(ids_h.size),
                 "vocab_size": V,
                 "global_batch": n_tok * world,
-                "parallelism": f"dp{world} (replicas + RCCL all-reduce average per step)" if world > 1 else "dp1",
+                "parallelism": (f"dp{world}: full replica per GPU, corpus shard per GPU, RCCL all-reduce "
+                                f"average x{rounds} per step" if world > 1 else "dp1"),
                 "kept_centers_per_step": int(delta["centers"] / args.steps),
                 "targets_per_step": int(delta["targets"] / args.steps),
             },

@@ -136,6 +136,10 @@ int w2v_dev_get_progress(w2v_dev* h, int64_t* current_words);
 int w2v_dev_train_epoch(w2v_dev* h, int32_t epoch, const int64_t* order, w2v_dev_stats* stats);
 /* The same, enqueued on the handle's stream; `order_dev` is a device array or NULL. */
 int w2v_dev_train_epoch_async(w2v_dev* h, int32_t epoch, const int64_t* order_dev);
+/* Train the `count` sentences listed in the device array `order_dev` (an
+ * arbitrary slice of an epoch's order), enqueued on the handle's stream: lets a
+ * caller cut an epoch into rounds between model-averaging points. */
+int w2v_dev_train_sentences_async(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int64_t count);
 int w2v_dev_synchronize(w2v_dev* h);
 int w2v_dev_read_stats(w2v_dev* h, w2v_dev_stats* stats); /* cumulative; synchronizes */
 int w2v_dev_reset_stats(w2v_dev* h);

@@ -79,6 +79,7 @@ SIGNATURES = {
     "w2v_dev_get_progress": (C.c_int, [_P, C.POINTER(_I64)]),
     "w2v_dev_train_epoch": (C.c_int, [_P, _I32, _P, C.POINTER(DevStats)]),
     "w2v_dev_train_epoch_async": (C.c_int, [_P, _I32, _P]),
+    "w2v_dev_train_sentences_async": (C.c_int, [_P, _I32, _P, _I64]),
     "w2v_dev_synchronize": (C.c_int, [_P]),
     "w2v_dev_read_stats": (C.c_int, [_P, C.POINTER(DevStats)]),
     "w2v_dev_reset_stats": (C.c_int, [_P]),

@@ -424,8 +424,21 @@ int w2v_dev_get_progress(w2v_dev* h, int64_t* cw) {
   return W2V_OK;
 }
 
+static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int64_t count);
+
 int w2v_dev_train_epoch_async(w2v_dev* h, int32_t epoch, const int64_t* order_dev) {
   if (!h) return fail(W2V_ERR_ARG, "null handle");
+  return launch_train(h, epoch, order_dev, h->n_sent);
+}
+
+int w2v_dev_train_sentences_async(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int64_t count) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (!order_dev && count != h->n_sent) return fail(W2V_ERR_ARG, "a slice needs an order array");
+  if (count < 0) return fail(W2V_ERR_ARG, "count < 0");
+  return launch_train(h, epoch, order_dev, count);
+}
+
+static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int64_t count) {
   if (!h->vocab_ready || !h->corpus_ready) return fail(W2V_ERR_STATE, "upload vocab and corpus first");
   if (!h->model_ready) return fail(W2V_ERR_STATE, "upload the model first");
   if (h->cfg.negative > 0 && !h->table) return fail(W2V_ERR_STATE, "no unigram table on the device");
@@ -435,7 +448,7 @@ int w2v_dev_train_epoch_async(w2v_dev* h, int32_t epoch, const int64_t* order_de
       return fail(W2V_ERR_ARG, "replay offsets do not cover this epoch");
   }
   if (epoch < 0) return fail(W2V_ERR_ARG, "epoch must be >= 0");
-  if (h->n_sent == 0) return W2V_OK;
+  if (count == 0) return W2V_OK;
   if (set_device(h)) return W2V_ERR_HIP;
   w2v::TrainArgs a;
   a.W = h->W; a.C = h->C; a.S = h->S;
@@ -443,7 +456,7 @@ int w2v_dev_train_epoch_async(w2v_dev* h, int32_t epoch, const int64_t* order_de
   a.window = h->cfg.window; a.negative = h->cfg.negative; a.cbow_mean = h->cfg.cbow_mean;
   a.iter = h->cfg.iter; a.init_alpha = h->cfg.init_alpha; a.min_alpha = h->cfg.min_alpha;
   a.train_words = (double)h->train_words;
-  a.ids = h->ids; a.soff = h->soff; a.order = order_dev; a.n_sent = h->n_sent;
+  a.ids = h->ids; a.soff = h->soff; a.order = order_dev; a.n_sent = count; a.n_corpus = h->n_sent;
   a.keep = h->keep; a.table = h->table; a.table_size = h->cfg.table_size;
   a.codes = h->codes; a.points = h->points; a.coff = h->coff;
   a.replay = h->replay;
@@ -462,7 +475,7 @@ int w2v_dev_train_epoch_async(w2v_dev* h, int32_t epoch, const int64_t* order_de
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0));
     if (per_cu < 1) per_cu = 1;
     const int64_t resident = (int64_t)per_cu * h->n_cu;
-    const int64_t need = (h->n_sent + 3) / 4;
+    const int64_t need = (count + 3) / 4;
     grid = dim3((unsigned)(need < resident ? need : resident));
     block = dim3(256);
   }

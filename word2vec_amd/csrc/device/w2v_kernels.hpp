@@ -54,8 +54,9 @@ struct TrainArgs {
   double train_words;
   const int32_t* ids;
   const int64_t* soff;
-  const int64_t* order;  // may be null (identity)
-  int64_t n_sent;
+  const int64_t* order;  // sentence ids to visit; null = identity over all sentences
+  int64_t n_sent;        // entries of `order` to process (work items)
+  int64_t n_corpus;      // sentences in the corpus (ids from `order` outside it are skipped)
   const float* keep;
   const uint32_t* table;
   int64_t table_size;
@@ -476,6 +477,7 @@ __global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
     k = (uint32_t)uniform_i((int)k);
     if ((int64_t)k >= a.n_sent) break;
     const int64_t s = a.order ? a.order[k] : (int64_t)k;
+    if (s < 0 || s >= a.n_corpus) continue;  // a caller-supplied device order is not host-checked
     if (a.fixed_alpha > 0.0f) {
       alpha = a.fixed_alpha;
     } else if (first || (k % 10u) == 0u) {

@@ -156,6 +156,11 @@ class DeviceTrainer:
                                                      C.c_void_p(order_dev_ptr) if order_dev_ptr else None),
                   "w2v_dev_train_epoch_async")
 
+    def train_sentences_async(self, epoch: int, order_dev_ptr: int, count: int):
+        """Train `count` sentences listed in a device int64 array (a slice of an epoch's order)."""
+        self._chk(self.lib.w2v_dev_train_sentences_async(self.h, int(epoch), C.c_void_p(order_dev_ptr), int(count)),
+                  "w2v_dev_train_sentences_async")
+
     def synchronize(self):
         self._chk(self.lib.w2v_dev_synchronize(self.h), "w2v_dev_synchronize")
 
