@@ -26,6 +26,8 @@ def test_analogy_on_additive_vectors():
     # the answer may never be one of the question words
     r2 = analogy_accuracy(["a", "b", "c"], np.eye(3), [("a", "b", "c", "a")])
     assert r2["accuracy"] == 0.0
+    r3 = analogy_accuracy(["a", "b", "c", "d"], np.eye(4), [("a", "b", "c", "a")])
+    assert r3["accuracy"] == 0.0
 
 
 def test_spearman_matches_scipy():

@@ -70,7 +70,9 @@ def analogy_accuracy(words: list[str], vecs: np.ndarray, questions, restrict: in
         for excl in (qa, qb, qc):
             ok = excl < cand.shape[0]
             sims[rows[ok], excl[ok]] = -np.inf
-        correct += int((sims.argmax(axis=1) == qd).sum())
+        best = sims.argmax(axis=1)
+        answerable = np.isfinite(sims[rows, best])  # every candidate excluded -> wrong
+        correct += int(((best == qd) & answerable).sum())
     return {"accuracy": 100.0 * correct / len(Q), "correct": correct, "answered": int(len(Q)),
             "skipped": len(questions) - int(len(Q))}
 
