@@ -15,7 +15,8 @@
  * handle's HIP stream (w2v_dev_set_stream).
  *
  * Device layout (HBM): W, C and synapses1 are row-major fp32 with a row pitch
- * of round_up(word_dim, 32) floats (128-B aligned rows); the unigram table is
+ * of round_up(word_dim, 32) floats (128-B aligned rows; a kernel lane owns
+ * elements lane + 64 v of a row); the unigram table is
  * uint32[table_size]; sample probabilities fp32[V]; Huffman paths are CSR
  * (uint8 codes, int32 points, int64 offsets); the corpus is int32 token ids
  * with int64 sentence offsets.
@@ -143,6 +144,16 @@ int w2v_dev_train_sentences_async(w2v_dev* h, int32_t epoch, const int64_t* orde
 int w2v_dev_synchronize(w2v_dev* h);
 int w2v_dev_read_stats(w2v_dev* h, w2v_dev_stats* stats); /* cumulative; synchronizes */
 int w2v_dev_reset_stats(w2v_dev* h);
+
+/* How row updates land (`row += g*x`, W[center] += grad, C[ctx] += grad):
+ * rows of W and C with index < hot_rows (the most frequent words: vocab is
+ * sorted by count) and the hot_rows internal Huffman nodes nearest the root
+ * use memory-side float atomic adds — no update is lost however many
+ * wavefronts hit the row; the other rows use a plain read-modify-write
+ * (lock-free Hogwild, an update racing another on the same row can be lost,
+ * as between the reference's OpenMP threads). -1 = every row atomic (the
+ * default), 0 = none. Same fp32 rounding either way. */
+int w2v_dev_set_hot_rows(w2v_dev* h, int64_t hot_rows);
 
 /* Word2Vec::train_sentence_* take alpha from the caller (Word2Vec.h:83-84):
  * alpha > 0 makes every following epoch use it instead of the schedule of

@@ -11,6 +11,25 @@
 
 #include "w2v_dev.h"
 #include "w2v_kernels.hpp"
+#include "w2v_launch.hpp"
+
+namespace w2v {
+
+// Expand the monotone unigram table from its V+1 first-index boundaries.
+__global__ void expand_table_kernel(const int64_t* bounds, int64_t V, uint32_t* table, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    int64_t lo = 0, hi = V - 1;  // largest w with bounds[w] <= i
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (bounds[mid] <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    table[i] = (uint32_t)lo;
+  }
+}
+
+}  // namespace w2v
 
 namespace {
 
@@ -44,7 +63,8 @@ struct w2v_dev {
   int64_t V = 0;
   int64_t pitch = 0;
   int32_t d4 = 0;
-  int vpl = 1;
+  int nv = 1;                 // floats per lane per row (instantiated width >= ceil(d / 64))
+  int64_t hot_rows = -1;      // rows updated with atomics: -1 = all, 0 = none
   bool need_C = false, need_S = false;
   float* W = nullptr;
   float* C = nullptr;
@@ -78,35 +98,45 @@ struct w2v_dev {
 
 namespace {
 
-constexpr int kMaxT = 8;
-
-using KernelFn = void (*)(w2v::TrainArgs);
-
-template <int VPL>
-KernelFn pick_kernel(bool cbow, bool hs, bool ns, bool replay) {
-#define W2V_K(CB, H, N, R) &w2v::train_epoch_kernel<VPL, kMaxT, CB, H, N, R>
-#define W2V_KR(CB, H, N) (replay ? W2V_K(CB, H, N, true) : W2V_K(CB, H, N, false))
-  if (cbow) {
-    if (hs && ns) return W2V_KR(true, true, true);
-    if (hs) return W2V_KR(true, true, false);
-    return W2V_KR(true, false, true);
-  }
-  if (hs && ns) return W2V_KR(false, true, true);
-  if (hs) return W2V_KR(false, true, false);
-  return W2V_KR(false, false, true);
-#undef W2V_KR
-#undef W2V_K
-}
+using KernelFn = w2v::KernelFn;
 
 KernelFn kernel_for(const w2v_dev* h) {
   const bool cb = h->cfg.cbow != 0, hs = h->cfg.hs != 0, ns = h->cfg.negative > 0;
   const bool rp = h->rng == W2V_RNG_REPLAY;
-  switch (h->vpl) {
-    case 1: return pick_kernel<1>(cb, hs, ns, rp);
-    case 2: return pick_kernel<2>(cb, hs, ns, rp);
-    case 3: return pick_kernel<3>(cb, hs, ns, rp);
-    default: return pick_kernel<4>(cb, hs, ns, rp);
+  switch (h->nv) {
+    case 1: return w2v::pick_train_nv1(cb, hs, ns, rp);
+    case 2: return w2v::pick_train_nv2(cb, hs, ns, rp);
+    case 3: return w2v::pick_train_nv3(cb, hs, ns, rp);
+    case 4: return w2v::pick_train_nv4(cb, hs, ns, rp);
+    case 5: return w2v::pick_train_nv5(cb, hs, ns, rp);
+    case 6: return w2v::pick_train_nv6(cb, hs, ns, rp);
+    case 8: return w2v::pick_train_nv8(cb, hs, ns, rp);
+    case 12: return w2v::pick_train_nv12(cb, hs, ns, rp);
+    default: return w2v::pick_train_nv16(cb, hs, ns, rp);
   }
+}
+
+w2v::ApplyFn apply_for(const w2v_dev* h) {
+  switch (h->nv) {
+    case 1: return w2v::pick_apply_nv1();
+    case 2: return w2v::pick_apply_nv2();
+    case 3: return w2v::pick_apply_nv3();
+    case 4: return w2v::pick_apply_nv4();
+    case 5: return w2v::pick_apply_nv5();
+    case 6: return w2v::pick_apply_nv6();
+    case 8: return w2v::pick_apply_nv8();
+    case 12: return w2v::pick_apply_nv12();
+    default: return w2v::pick_apply_nv16();
+  }
+}
+
+// Instantiated row widths (floats per lane): the smallest one covering d.
+int pick_nv(int d) {
+  const int need = (d + w2v::kWave - 1) / w2v::kWave;
+  static const int widths[] = {1, 2, 3, 4, 5, 6, 8, 12, 16};
+  for (int w : widths)
+    if (w >= need) return w;
+  return 16;
 }
 
 int set_device(w2v_dev* h) {
@@ -161,7 +191,7 @@ int w2v_dev_create(const w2v_dev_config* cfg, w2v_dev** out) {
   h->n_cu = ncu > 0 ? ncu : 256;
   h->d4 = (cfg->word_dim + 3) & ~3;
   h->pitch = (cfg->word_dim + 31) & ~31;
-  h->vpl = (h->d4 / 4 + w2v::kWave - 1) / w2v::kWave;
+  h->nv = pick_nv(cfg->word_dim);
   h->need_C = cfg->negative > 0 || cfg->cbow;
   h->need_S = cfg->hs != 0;
   *out = h;
@@ -452,7 +482,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   if (set_device(h)) return W2V_ERR_HIP;
   w2v::TrainArgs a;
   a.W = h->W; a.C = h->C; a.S = h->S;
-  a.pitch = h->pitch; a.d4 = h->d4;
+  a.pitch = h->pitch; a.dim = h->cfg.word_dim;
   a.window = h->cfg.window; a.negative = h->cfg.negative; a.cbow_mean = h->cfg.cbow_mean;
   a.iter = h->cfg.iter; a.init_alpha = h->cfg.init_alpha; a.min_alpha = h->cfg.min_alpha;
   a.train_words = (double)h->train_words;
@@ -467,6 +497,12 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   a.key0 = (uint32_t)h->seed; a.key1 = (uint32_t)(h->seed >> 32);
   a.epoch = (uint32_t)epoch;
   a.fixed_alpha = h->fixed_alpha;
+  {
+    const int64_t hot = h->hot_rows < 0 ? h->V : (h->hot_rows < h->V ? h->hot_rows : h->V);
+    a.hot_wc = hot;
+    a.hot_s = (h->V - 1) - hot;  // the top `hot` internal nodes (the root is V-2)
+  }
+  a.strict = h->sched == W2V_SCHED_SEQUENTIAL ? 1 : 0;
   KernelFn fn = kernel_for(h);
   HIP_TRY(hipMemsetAsync(h->work, 0, sizeof(unsigned int), h->stream));
   dim3 grid(1), block(64);
@@ -546,6 +582,13 @@ int w2v_dev_reset_stats(w2v_dev* h) {
   return W2V_OK;
 }
 
+int w2v_dev_set_hot_rows(w2v_dev* h, int64_t hot_rows) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (hot_rows < -1) return fail(W2V_ERR_ARG, "hot_rows must be >= -1");
+  h->hot_rows = hot_rows;
+  return W2V_OK;
+}
+
 int w2v_dev_set_fixed_alpha(w2v_dev* h, float alpha) {
   if (!h) return fail(W2V_ERR_ARG, "null handle");
   h->fixed_alpha = alpha > 0 ? alpha : 0.0f;
@@ -575,15 +618,9 @@ int w2v_dev_apply_rows(w2v_dev* h, float* rows, const uint8_t* codes, int32_t n,
     HIP_TRY(hipMemcpy2DAsync(dr, dp, rows, d * sizeof(float), d * sizeof(float), n, hipMemcpyHostToDevice, h->stream));
     HIP_TRY(hipMemcpyAsync(h->scratch_codes, codes, n, hipMemcpyHostToDevice, h->stream));
   }
-  void (*fn)(float*, int64_t, int, const float*, float*, const uint8_t*, int, float, int);
-  switch (h->vpl) {
-    case 1: fn = &w2v::apply_rows_kernel<1>; break;
-    case 2: fn = &w2v::apply_rows_kernel<2>; break;
-    case 3: fn = &w2v::apply_rows_kernel<3>; break;
-    default: fn = &w2v::apply_rows_kernel<4>; break;
-  }
-  hipLaunchKernelGGL(fn, dim3(1), dim3(64), 0, h->stream, dr, h->pitch, h->d4, dx, dg, h->scratch_codes, n,
-                     alpha, hs_form);
+  w2v::ApplyFn fn = apply_for(h);
+  hipLaunchKernelGGL(fn, dim3(1), dim3(64), 0, h->stream, dr, h->pitch, h->cfg.word_dim, dx, dg, h->scratch_codes,
+                     n, alpha, hs_form);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(grad, dg, d * sizeof(float), hipMemcpyDeviceToHost, h->stream));
   if (n > 0)

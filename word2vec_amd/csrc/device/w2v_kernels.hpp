@@ -17,20 +17,28 @@
 //     sentences from a global head counter (Hogwild across sentences, as the
 //     reference is across threads). A one-wave grid is the deterministic
 //     sequential schedule used for parity.
-//   * an embedding row is spread over the wave as float4 lanes (lane l holds
-//     elements 4l..4l+3, 4(l+64)..): every row gather/scatter is one or a few
-//     fully coalesced 1-KiB wave instructions; the rows of all targets of one
-//     context (<= MAXT) are gathered together for memory-level parallelism.
+//   * an embedding row is spread over the wave one dword per lane per 64
+//     elements (element lane + 64 v): every row gather is NV fully coalesced
+//     256-B wave instructions, and a row update is NV 256-B contiguous
+//     instructions — the shape at which MI355X float atomics run at full rate.
+//     The rows of all targets of one context (<= MAXT) are gathered together.
 //   * dot products reduce across the wave with DPP (row rotations + row
 //     broadcasts, no LDS), the result read back with v_readlane into an SGPR,
 //     so the sigmoid and gradient scalar are wave-uniform.
-//   * axpy scatter-back is plain (lock-free, Hogwild) 16-B stores.
+//   * updates `row += g * x` (and W[center] += grad, C[ctx] += grad) are
+//     either plain stores of the updated row (lock-free Hogwild) or memory-side
+//     global_atomic_add_f32 of g * x — the same fp32 rounding as the
+//     reference's `row = row + g*x`, but no update is lost when thousands of
+//     wavefronts hit one row. Rows inside the "hot" range (frequent words: the
+//     low vocab indices, the top of the Huffman tree) take the atomic path;
+//     their gathers use L1-bypassing agent-scope loads so a wavefront sees its
+//     own atomics. Per-XCD L2s are not coherent inside a launch, so what
+//     another XCD wrote may be read late (delayed SGD) but is never lost.
 //   * Philox4x32-10 counter-based draws make every random decision a pure
-//     function of (key, epoch, sentence, position, slot, k), so the parallel
-//     schedule needs no shared generator; in Philox mode subsampling decisions
-//     for 64 tokens are made at once (one lane per token) and only kept centers
-//     are walked. Replay mode instead consumes the reference's own mt19937
-//     stream recorded on the host, in the reference's draw order.
+//     function of (key, epoch, sentence, position, slot, k); in Philox mode
+//     subsampling decisions for 64 tokens are made at once (one lane per
+//     token) and only kept centers are walked. Replay mode consumes the
+//     reference's own mt19937 stream recorded on the host, in its draw order.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -43,8 +51,8 @@ struct TrainArgs {
   float* W;
   float* C;
   float* S;             // synapses1
-  int64_t pitch;        // row pitch in floats (multiple of 32)
-  int32_t d4;           // word_dim rounded up to a multiple of 4
+  int64_t pitch;        // row pitch in floats (multiple of 4)
+  int32_t dim;          // word_dim
   int32_t window;
   int32_t negative;
   int32_t cbow_mean;
@@ -70,6 +78,9 @@ struct TrainArgs {
   unsigned long long* stats;   // centers, contexts, targets, draws, sentences
   uint32_t key0, key1, epoch;
   float fixed_alpha;           // > 0: use instead of the schedule
+  int64_t hot_wc;              // W / C rows [0, hot_wc) update with atomics
+  int64_t hot_s;               // synapses1 rows [hot_s, V-1) update with atomics
+  int32_t strict;              // 1: drain own atomics before re-reading (sequential schedule)
 };
 
 struct Counters {
@@ -101,6 +112,9 @@ __device__ __forceinline__ int readlane_i(int v, int l) { return __builtin_amdgc
 __device__ __forceinline__ int uniform_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 __device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
+
+// Wait until this wave's outstanding memory operations (incl. no-return atomics) completed.
+__device__ __forceinline__ void drain_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // ---------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al. SC'11), the throughput-mode RNG.
@@ -135,43 +149,57 @@ __device__ __forceinline__ uint32_t philox_table_pos(const TrainArgs& a, uint32_
 }
 
 // ---------------------------------------------------------------------------
-// Row I/O: a row is VPL float4 per lane, element 4*(lane + 64 v).
+// Row I/O: a row is NV floats per lane, element lane + 64 v (v < NV).
 // ---------------------------------------------------------------------------
-template <int VPL>
-__device__ __forceinline__ void load_row(const float* M, int64_t row, int64_t pitch, int d4,
-                                         int lane, float4 (&r)[VPL]) {
-  const float* p = M + row * pitch;
+template <int NV>
+__device__ __forceinline__ void load_row(const float* M, int64_t row, int64_t pitch, int d, int lane,
+                                         bool fresh, float (&r)[NV]) {
+  const float* p = M + row * pitch + lane;
+  if (fresh) {  // agent-scope relaxed loads: global_load_dword sc1, bypass the CU's L1
 #pragma unroll
-  for (int v = 0; v < VPL; ++v) {
-    const int e = 4 * (lane + kWave * v);
-    r[v] = (e < d4) ? *reinterpret_cast<const float4*>(p + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int v = 0; v < NV; ++v)
+      r[v] = (lane + kWave * v < d)
+                 ? __hip_atomic_load(p + kWave * v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                 : 0.f;
+  } else {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) r[v] = (lane + kWave * v < d) ? p[kWave * v] : 0.f;
   }
 }
 
-template <int VPL>
-__device__ __forceinline__ void store_row(float* M, int64_t row, int64_t pitch, int d4, int lane,
-                                          const float4 (&r)[VPL]) {
-  float* p = M + row * pitch;
+template <int NV>
+__device__ __forceinline__ void store_row(float* M, int64_t row, int64_t pitch, int d, int lane,
+                                          const float (&r)[NV]) {
+  float* p = M + row * pitch + lane;
 #pragma unroll
-  for (int v = 0; v < VPL; ++v) {
-    const int e = 4 * (lane + kWave * v);
-    if (e < d4) *reinterpret_cast<float4*>(p + e) = r[v];
+  for (int v = 0; v < NV; ++v)
+    if (lane + kWave * v < d) p[kWave * v] = r[v];
+}
+
+// row += delta, memory-side (no-return global_atomic_add_f32, 256 contiguous B per instruction)
+template <int NV>
+__device__ __forceinline__ void atomic_add_row(float* M, int64_t row, int64_t pitch, int d, int lane,
+                                               const float (&delta)[NV]) {
+  float* p = M + row * pitch + lane;
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+    if (lane + kWave * v < d)
+      (void)__hip_atomic_fetch_add(p + kWave * v, delta[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// M[row] += delta: atomically for hot rows; else read-modify-write (Hogwild).
+template <int NV>
+__device__ __forceinline__ void add_to_row(float* M, int64_t row, bool hot, int64_t pitch, int d, int lane,
+                                           const float (&delta)[NV]) {
+  if (hot) {
+    atomic_add_row<NV>(M, row, pitch, d, lane, delta);
+  } else {
+    float cur[NV];
+    load_row<NV>(M, row, pitch, d, lane, false, cur);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) cur[v] += delta[v];
+    store_row<NV>(M, row, pitch, d, lane, cur);
   }
-}
-
-__device__ __forceinline__ float dot4(const float4 a, const float4 b) {
-  float s = a.x * b.x;
-  s += a.y * b.y;
-  s += a.z * b.z;
-  s += a.w * b.w;
-  return s;
-}
-
-__device__ __forceinline__ void axpy4(float4& y, float g, const float4 x) {
-  y.x += g * x.x;
-  y.y += g * x.y;
-  y.z += g * x.z;
-  y.w += g * x.w;
 }
 
 // ---------------------------------------------------------------------------
@@ -179,18 +207,20 @@ __device__ __forceinline__ void axpy4(float4& y, float g, const float4 x) {
 // MAXT distinct rows at once. Lane (t0 + t) of row_l / code_l holds target t's
 // row and code (HS: Huffman code; NS: 1 - label). Rows are gathered together,
 // then updated in target order so grad accumulates in the reference's order.
+// Rows in [hot_lo, hot_hi) take the atomic path.
 // ---------------------------------------------------------------------------
-template <int VPL, int MAXT, bool HSF>
-__device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d4, int lane, int T,
-                                              int row_l, int code_l, int t0,
-                                              const float4 (&x)[VPL], float4 (&g)[VPL],
-                                              float alpha) {
-  float4 r[MAXT][VPL];
+template <int NV, int MAXT, bool HSF>
+__device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, int lane, int T, int row_l,
+                                              int code_l, int t0, const float (&x)[NV], float (&g)[NV],
+                                              float alpha, int64_t hot_lo, int64_t hot_hi) {
+  float r[MAXT][NV];
   int rows[MAXT];
+  bool hot[MAXT];
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) {
     rows[t] = readlane_i(row_l, t0 + t);
-    if (t < T) load_row<VPL>(M, rows[t], pitch, d4, lane, r[t]);
+    hot[t] = rows[t] >= hot_lo && rows[t] < hot_hi;
+    if (t < T) load_row<NV>(M, rows[t], pitch, d, lane, hot[t], r[t]);
   }
   float f[MAXT];
 #pragma unroll
@@ -199,7 +229,7 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d4, i
     if (t < T) {
       float p = 0.f;
 #pragma unroll
-      for (int v = 0; v < VPL; ++v) p += dot4(r[t][v], x[v]);
+      for (int v = 0; v < NV; ++v) p += r[t][v] * x[v];
       f[t] = wave_sum(p);
     }
   }
@@ -216,30 +246,38 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d4, i
         const float s = (float)(1.0 / (double)(1.0f + e));
         gt = ((float)(1 - code) - s) * alpha;
       }
+      float delta[NV];
 #pragma unroll
-      for (int v = 0; v < VPL; ++v) {
-        axpy4(g[v], gt, r[t][v]);
-        axpy4(r[t][v], gt, x[v]);
+      for (int v = 0; v < NV; ++v) {
+        g[v] += gt * r[t][v];  // grad uses the pre-update row (:244 / :266)
+        delta[v] = gt * x[v];
       }
-      store_row<VPL>(M, rows[t], pitch, d4, lane, r[t]);
+      if (hot[t]) {
+        atomic_add_row<NV>(M, rows[t], pitch, d, lane, delta);
+      } else {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) r[t][v] += delta[v];
+        store_row<NV>(M, rows[t], pitch, d, lane, r[t]);
+      }
     }
   }
 }
 
 // HS on the path of `word` (synapses1 rows).
-template <int VPL, int MAXT>
-__device__ __forceinline__ void hs_word(const TrainArgs& a, int word, int lane,
-                                        const float4 (&x)[VPL], float4 (&g)[VPL], float alpha,
-                                        Counters& cnt) {
+template <int NV, int MAXT>
+__device__ __forceinline__ void hs_word(const TrainArgs& a, int word, int lane, const float (&x)[NV],
+                                        float (&g)[NV], float alpha, Counters& cnt) {
   const int64_t cb = a.coff[word];
   const int L = (int)(a.coff[word + 1] - cb);
   for (int c0 = 0; c0 < L; c0 += kWave) {
     const int rem = min(kWave, L - c0);
     const int pt_l = (lane < rem) ? a.points[cb + c0 + lane] : 0;
     const int cd_l = (lane < rem) ? (int)a.codes[cb + c0 + lane] : 0;
-    for (int t0 = 0; t0 < rem; t0 += MAXT)
-      apply_targets<VPL, MAXT, true>(a.S, a.pitch, a.d4, lane, min(MAXT, rem - t0), pt_l, cd_l,
-                                     t0, x, g, alpha);
+    for (int t0 = 0; t0 < rem; t0 += MAXT) {
+      if (a.strict) drain_vmem();
+      apply_targets<NV, MAXT, true>(a.S, a.pitch, a.dim, lane, min(MAXT, rem - t0), pt_l, cd_l, t0, x, g,
+                                    alpha, a.hot_s, INT64_MAX);
+    }
     cnt.targets += (unsigned long long)rem;
   }
 }
@@ -247,10 +285,9 @@ __device__ __forceinline__ void hs_word(const TrainArgs& a, int word, int lane,
 // NS with positive `word` against `negw_l` lanes [base, base + neg): builds the
 // target list (positive first, then first occurrences of the negatives that
 // differ from it — the set semantics of Word2Vec.cpp:253-257) and applies it.
-template <int VPL, int MAXT>
-__device__ __forceinline__ void ns_word(const TrainArgs& a, float* M, int word, int negw_l,
-                                        int base, int lane, const float4 (&x)[VPL],
-                                        float4 (&g)[VPL], float alpha, Counters& cnt) {
+template <int NV, int MAXT>
+__device__ __forceinline__ void ns_word(const TrainArgs& a, float* M, int word, int negw_l, int base, int lane,
+                                        const float (&x)[NV], float (&g)[NV], float alpha, Counters& cnt) {
   const int neg = a.negative;
   const int nk = __shfl(negw_l, (base + lane) & (kWave - 1));
   bool dup = (lane >= neg) || (nk == word);
@@ -270,18 +307,19 @@ __device__ __forceinline__ void ns_word(const TrainArgs& a, float* M, int word, 
   }
   const int T = m;
   const int code_l = (lane == 0) ? 0 : 1;
-  for (int t0 = 0; t0 < T; t0 += MAXT)
-    apply_targets<VPL, MAXT, false>(M, a.pitch, a.d4, lane, min(MAXT, T - t0), tgt_l, code_l, t0,
-                                    x, g, alpha);
+  for (int t0 = 0; t0 < T; t0 += MAXT) {
+    if (a.strict) drain_vmem();
+    apply_targets<NV, MAXT, false>(M, a.pitch, a.dim, lane, min(MAXT, T - t0), tgt_l, code_l, t0, x, g, alpha,
+                                   0, a.hot_wc);
+  }
   cnt.targets += (unsigned long long)T;
 }
 
-// Draw table words for `cnt_draws` (slot, k) pairs starting at slot `slot0`:
+// Draw table words for `ndraw` (slot, k) pairs starting at slot `slot0`:
 // lane t -> slot0 + t / neg, k = t % neg.
 template <bool REPLAY>
-__device__ __forceinline__ int draw_negatives(const TrainArgs& a, uint32_t s, uint32_t i,
-                                              int slot0, int ndraw, int lane,
-                                              const uint32_t*& rp) {
+__device__ __forceinline__ int draw_negatives(const TrainArgs& a, uint32_t s, uint32_t i, int slot0, int ndraw,
+                                              int lane, const uint32_t*& rp) {
   int w = 0;
   if (lane < ndraw) {
     uint32_t pos;
@@ -300,16 +338,17 @@ __device__ __forceinline__ int draw_negatives(const TrainArgs& a, uint32_t s, ui
 // ---------------------------------------------------------------------------
 // Skip-gram center (Word2Vec.cpp:329-351) with its window [lo, hi).
 // ---------------------------------------------------------------------------
-template <int VPL, int MAXT, bool HS, bool NS, bool REPLAY>
-__device__ __forceinline__ void sg_center(const TrainArgs& a, const int32_t* sent, int len, int i,
-                                          int c, int rw, uint32_t s, float alpha,
-                                          const uint32_t*& rp, Counters& cnt, int lane) {
+template <int NV, int MAXT, bool HS, bool NS, bool REPLAY>
+__device__ __forceinline__ void sg_center(const TrainArgs& a, const int32_t* sent, int len, int i, int c, int rw,
+                                          uint32_t s, float alpha, const uint32_t*& rp, Counters& cnt, int lane) {
   const int lo = max(0, i - a.window + rw), hi = min(len, i + a.window + 1 - rw);
   const int span = hi - lo;
-  float4 x[VPL], g[VPL];
-  load_row<VPL>(a.W, c, a.pitch, a.d4, lane, x);
+  const bool hot_c = c < a.hot_wc;
+  float x[NV], g[NV];
+  if (a.strict) drain_vmem();
+  load_row<NV>(a.W, c, a.pitch, a.dim, lane, hot_c, x);
 #pragma unroll
-  for (int v = 0; v < VPL; ++v) g[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int v = 0; v < NV; ++v) g[v] = 0.f;
   const int ctx_l = (lane < span) ? sent[lo + lane] : 0;
   cnt.centers += 1;
   cnt.contexts += (unsigned long long)(span - 1);
@@ -321,7 +360,7 @@ __device__ __forceinline__ void sg_center(const TrainArgs& a, const int32_t* sen
   for (int j = lo; j < hi; ++j) {
     if (j == i) continue;
     const int w = readlane_i(ctx_l, j - lo);
-    if (HS) hs_word<VPL, MAXT>(a, w, lane, x, g, alpha, cnt);
+    if (HS) hs_word<NV, MAXT>(a, w, lane, x, g, alpha, cnt);
     if (NS) {
       const int gs = slot % G;
       if (gs == 0) {
@@ -329,29 +368,19 @@ __device__ __forceinline__ void sg_center(const TrainArgs& a, const int32_t* sen
         negw_l = draw_negatives<REPLAY>(a, s, (uint32_t)i, slot, nd, lane, rp);
         cnt.draws += (unsigned long long)nd;
       }
-      ns_word<VPL, MAXT>(a, a.C, w, negw_l, gs * neg, lane, x, g, alpha, cnt);
+      ns_word<NV, MAXT>(a, a.C, w, negw_l, gs * neg, lane, x, g, alpha, cnt);
     }
     ++slot;
   }
-  float4 cur[VPL];
-  load_row<VPL>(a.W, c, a.pitch, a.d4, lane, cur);
-#pragma unroll
-  for (int v = 0; v < VPL; ++v) {
-    cur[v].x += g[v].x;
-    cur[v].y += g[v].y;
-    cur[v].z += g[v].z;
-    cur[v].w += g[v].w;
-  }
-  store_row<VPL>(a.W, c, a.pitch, a.d4, lane, cur);
+  add_to_row<NV>(a.W, c, hot_c, a.pitch, a.dim, lane, g);  // W.row(center) += neu1_grad (:351)
 }
 
 // ---------------------------------------------------------------------------
 // CBOW center (Word2Vec.cpp:286-315).
 // ---------------------------------------------------------------------------
-template <int VPL, int MAXT, bool HS, bool NS, bool REPLAY>
-__device__ __forceinline__ void cbow_center(const TrainArgs& a, const int32_t* sent, int len,
-                                            int i, int c, int rw, uint32_t s, float alpha,
-                                            const uint32_t*& rp, Counters& cnt, int lane) {
+template <int NV, int MAXT, bool HS, bool NS, bool REPLAY>
+__device__ __forceinline__ void cbow_center(const TrainArgs& a, const int32_t* sent, int len, int i, int c, int rw,
+                                            uint32_t s, float alpha, const uint32_t*& rp, Counters& cnt, int lane) {
   const int lo = max(0, i - a.window + rw), hi = min(len, i + a.window + 1 - rw);
   const int n = hi - lo - 1;  // neu1_num, positional
   if (n <= 0) return;
@@ -388,83 +417,60 @@ __device__ __forceinline__ void cbow_center(const TrainArgs& a, const int32_t* s
   }
   cnt.centers += 1;
   cnt.contexts += (unsigned long long)U;
-  float4 h[VPL], g[VPL];
+  float h[NV], g[NV];
 #pragma unroll
-  for (int v = 0; v < VPL; ++v) {
-    h[v] = make_float4(0.f, 0.f, 0.f, 0.f);
-    g[v] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
+  for (int v = 0; v < NV; ++v) h[v] = g[v] = 0.f;
+  if (a.strict) drain_vmem();
   for (int r0 = 0; r0 < U; r0 += MAXT) {
-    float4 rr[MAXT][VPL];
+    float rr[MAXT][NV];
 #pragma unroll
     for (int t = 0; t < MAXT; ++t)
-      if (r0 + t < U) load_row<VPL>(a.C, readlane_i(sid, r0 + t), a.pitch, a.d4, lane, rr[t]);
+      if (r0 + t < U) {
+        const int row = readlane_i(sid, r0 + t);
+        load_row<NV>(a.C, row, a.pitch, a.dim, lane, row < a.hot_wc, rr[t]);
+      }
 #pragma unroll
     for (int t = 0; t < MAXT; ++t)
       if (r0 + t < U) {
 #pragma unroll
-        for (int v = 0; v < VPL; ++v) {
-          h[v].x += rr[t][v].x;
-          h[v].y += rr[t][v].y;
-          h[v].z += rr[t][v].z;
-          h[v].w += rr[t][v].w;
-        }
+        for (int v = 0; v < NV; ++v) h[v] += rr[t][v];
       }
   }
   const float nf = (float)n;
   if (a.cbow_mean) {
 #pragma unroll
-    for (int v = 0; v < VPL; ++v) {
-      h[v].x /= nf; h[v].y /= nf; h[v].z /= nf; h[v].w /= nf;
-    }
+    for (int v = 0; v < NV; ++v) h[v] /= nf;
   }
-  if (HS) hs_word<VPL, MAXT>(a, c, lane, h, g, alpha, cnt);
+  if (HS) hs_word<NV, MAXT>(a, c, lane, h, g, alpha, cnt);
   if (NS) {
     const int nd = a.negative;
     const int negw_l = draw_negatives<REPLAY>(a, s, (uint32_t)i, 0, nd, lane, rp);
     cnt.draws += (unsigned long long)nd;
-    ns_word<VPL, MAXT>(a, a.W, c, negw_l, 0, lane, h, g, alpha, cnt);
+    ns_word<NV, MAXT>(a, a.W, c, negw_l, 0, lane, h, g, alpha, cnt);
   }
   if (a.cbow_mean) {
 #pragma unroll
-    for (int v = 0; v < VPL; ++v) {
-      g[v].x /= nf; g[v].y /= nf; g[v].z /= nf; g[v].w /= nf;
-    }
+    for (int v = 0; v < NV; ++v) g[v] /= nf;
   }
-  for (int r0 = 0; r0 < U; r0 += MAXT) {
-    float4 rr[MAXT][VPL];
-#pragma unroll
-    for (int t = 0; t < MAXT; ++t)
-      if (r0 + t < U) load_row<VPL>(a.C, readlane_i(sid, r0 + t), a.pitch, a.d4, lane, rr[t]);
-#pragma unroll
-    for (int t = 0; t < MAXT; ++t)
-      if (r0 + t < U) {
-#pragma unroll
-        for (int v = 0; v < VPL; ++v) {
-          rr[t][v].x += g[v].x;
-          rr[t][v].y += g[v].y;
-          rr[t][v].z += g[v].z;
-          rr[t][v].w += g[v].w;
-        }
-        store_row<VPL>(a.C, readlane_i(sid, r0 + t), a.pitch, a.d4, lane, rr[t]);
-      }
+  for (int r = 0; r < U; ++r) {  // C.row(id) += neu1_grad for every unique id (:315)
+    const int row = readlane_i(sid, r);
+    add_to_row<NV>(a.C, row, row < a.hot_wc, a.pitch, a.dim, lane, g);
   }
 }
 
-template <int VPL, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY>
-__device__ __forceinline__ void center(const TrainArgs& a, const int32_t* sent, int len, int i,
-                                       int c, int rw, uint32_t s, float alpha,
-                                       const uint32_t*& rp, Counters& cnt, int lane) {
+template <int NV, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY>
+__device__ __forceinline__ void center(const TrainArgs& a, const int32_t* sent, int len, int i, int c, int rw,
+                                       uint32_t s, float alpha, const uint32_t*& rp, Counters& cnt, int lane) {
   if (CBOW)
-    cbow_center<VPL, MAXT, HS, NS, REPLAY>(a, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
+    cbow_center<NV, MAXT, HS, NS, REPLAY>(a, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
   else
-    sg_center<VPL, MAXT, HS, NS, REPLAY>(a, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
+    sg_center<NV, MAXT, HS, NS, REPLAY>(a, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
 }
 
 // ---------------------------------------------------------------------------
 // The epoch kernel: wavefronts dequeue sentences (Word2Vec.cpp:375-394).
 // ---------------------------------------------------------------------------
-template <int VPL, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY>
+template <int NV, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY>
 __global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
   const int lane = lane_id();
   Counters cnt;
@@ -481,10 +487,8 @@ __global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
     if (a.fixed_alpha > 0.0f) {
       alpha = a.fixed_alpha;
     } else if (first || (k % 10u) == 0u) {
-      const unsigned long long cw =
-          __hip_atomic_load(a.words, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const float al =
-          (float)(a.init_alpha * (1.0 - 1.0 / a.iter * (double)cw / a.train_words));
+      const unsigned long long cw = __hip_atomic_load(a.words, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float al = (float)(a.init_alpha * (1.0 - 1.0 / a.iter * (double)cw / a.train_words));
       alpha = (a.min_alpha < al) ? al : a.min_alpha;
       first = false;
     }
@@ -501,8 +505,7 @@ __global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
         if (a.keep[c] < u) continue;
         const int rw = (int)rp[0];
         ++rp;
-        center<VPL, MAXT, CBOW, HS, NS, REPLAY>(a, sent, len, i, c, rw, (uint32_t)s, alpha, rp,
-                                                cnt, lane);
+        center<NV, MAXT, CBOW, HS, NS, REPLAY>(a, sent, len, i, c, rw, (uint32_t)s, alpha, rp, cnt, lane);
       }
     } else {
       for (int i0 = 0; i0 < len; i0 += kWave) {
@@ -519,8 +522,7 @@ __global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
           const int b = __builtin_ctzll(kept);
           kept &= kept - 1;
           const int c = readlane_i(c_l, b), rw = readlane_i(rw_l, b);
-          center<VPL, MAXT, CBOW, HS, NS, REPLAY>(a, sent, len, i0 + b, c, rw, (uint32_t)s,
-                                                  alpha, rp, cnt, lane);
+          center<NV, MAXT, CBOW, HS, NS, REPLAY>(a, sent, len, i0 + b, c, rw, (uint32_t)s, alpha, rp, cnt, lane);
         }
       }
     }
@@ -537,44 +539,30 @@ __global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
 }
 
 // Sequential target updates for w2v_dev_apply_rows (one wave): target t is
-// row t of M, applied in order (rows are distinct).
-template <int VPL>
-__global__ __launch_bounds__(64) void apply_rows_kernel(float* M, int64_t pitch, int d4, const float* x_in,
+// row t of M, applied in order (rows are distinct; plain read-modify-write).
+template <int NV>
+__global__ __launch_bounds__(64) void apply_rows_kernel(float* M, int64_t pitch, int d, const float* x_in,
                                                         float* grad_io, const uint8_t* codes, int n, float alpha,
                                                         int hs_form) {
   const int lane = lane_id();
-  float4 x[VPL], g[VPL];
+  float x[NV], g[NV];
 #pragma unroll
-  for (int v = 0; v < VPL; ++v) {
-    const int e = 4 * (lane + kWave * v);
-    x[v] = (e < d4) ? *reinterpret_cast<const float4*>(x_in + e) : make_float4(0.f, 0.f, 0.f, 0.f);
-    g[v] = (e < d4) ? *reinterpret_cast<const float4*>(grad_io + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int v = 0; v < NV; ++v) {
+    const int e = lane + kWave * v;
+    x[v] = (e < d) ? x_in[e] : 0.f;
+    g[v] = (e < d) ? grad_io[e] : 0.f;
   }
   for (int t = 0; t < n; ++t) {
     const int code = (int)codes[t];
     if (hs_form)
-      apply_targets<VPL, 1, true>(M, pitch, d4, lane, 1, t, code, 0, x, g, alpha);
+      apply_targets<NV, 1, true>(M, pitch, d, lane, 1, t, code, 0, x, g, alpha, 0, 0);
     else
-      apply_targets<VPL, 1, false>(M, pitch, d4, lane, 1, t, code, 0, x, g, alpha);
+      apply_targets<NV, 1, false>(M, pitch, d, lane, 1, t, code, 0, x, g, alpha, 0, 0);
   }
 #pragma unroll
-  for (int v = 0; v < VPL; ++v) {
-    const int e = 4 * (lane + kWave * v);
-    if (e < d4) *reinterpret_cast<float4*>(grad_io + e) = g[v];
-  }
-}
-
-// Expand the monotone unigram table from its V+1 first-index boundaries.
-__global__ void expand_table_kernel(const int64_t* bounds, int64_t V, uint32_t* table, int64_t n) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    int64_t lo = 0, hi = V - 1;  // largest w with bounds[w] <= i
-    while (lo < hi) {
-      const int64_t mid = (lo + hi + 1) >> 1;
-      if (bounds[mid] <= i) lo = mid;
-      else hi = mid - 1;
-    }
-    table[i] = (uint32_t)lo;
+  for (int v = 0; v < NV; ++v) {
+    const int e = lane + kWave * v;
+    if (e < d) grad_io[e] = g[v];
   }
 }
 

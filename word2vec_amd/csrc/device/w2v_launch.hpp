@@ -1,0 +1,25 @@
+// Kernel entry points per row width (defined in w2v_inst.hip, one object per width).
+#pragma once
+#include <stdint.h>
+
+namespace w2v {
+
+struct TrainArgs;
+using KernelFn = void (*)(TrainArgs);
+using ApplyFn = void (*)(float*, int64_t, int, const float*, float*, const uint8_t*, int, float, int);
+
+#define W2V_DECLARE_NV(N)                                            \
+  KernelFn pick_train_nv##N(bool cbow, bool hs, bool ns, bool replay); \
+  ApplyFn pick_apply_nv##N();
+W2V_DECLARE_NV(1)
+W2V_DECLARE_NV(2)
+W2V_DECLARE_NV(3)
+W2V_DECLARE_NV(4)
+W2V_DECLARE_NV(5)
+W2V_DECLARE_NV(6)
+W2V_DECLARE_NV(8)
+W2V_DECLARE_NV(12)
+W2V_DECLARE_NV(16)
+#undef W2V_DECLARE_NV
+
+}  // namespace w2v

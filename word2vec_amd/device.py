@@ -172,6 +172,10 @@ class DeviceTrainer:
     def reset_stats(self):
         self._chk(self.lib.w2v_dev_reset_stats(self.h), "w2v_dev_reset_stats")
 
+    def set_hot_rows(self, hot_rows: int):
+        """Rows updated with atomics: -1 = all (default), 0 = none (plain Hogwild RMW), k = the k most frequent."""
+        self._chk(self.lib.w2v_dev_set_hot_rows(self.h, int(hot_rows)), "w2v_dev_set_hot_rows")
+
     def set_fixed_alpha(self, alpha: float):
         self._chk(self.lib.w2v_dev_set_fixed_alpha(self.h, float(alpha)), "w2v_dev_set_fixed_alpha")
 
