@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--hot-rows", type=int, default=-1,
                     help="rows updated with atomics (-1 all, 0 none = plain Hogwild RMW, k = k most frequent)")
+    ap.add_argument("--private-rows", type=int, default=-1,
+                    help="hottest output rows privatised per workgroup in LDS (-1 auto, 0 off)")
     ap.add_argument("--sync-every", type=int, default=0,
                     help="average the replicas every this many sentences of a shard (0 = once per step)")
     return ap.parse_args()
@@ -164,6 +166,7 @@ def main():
     tr.set_rng(N.W2V_RNG_PHILOX, (args.seed << 32) | (rank + 1))
     tr.set_schedule(N.W2V_SCHED_PARALLEL)
     tr.set_hot_rows(args.hot_rows)
+    tr.set_private_rows(args.private_rows)
     tr.set_progress(0)
     torch.cuda.synchronize()
     log(f"[bench] resident in HBM ({time.time() - t0:.1f}s)")
@@ -256,6 +259,7 @@ def main():
                 "parallelism": (f"dp{world}: full replica per GPU, corpus shard per GPU, RCCL all-reduce "
                                 f"average x{rounds} per step" if world > 1 else "dp1"),
                 "hot_rows": args.hot_rows,
+                "private_rows": args.private_rows,
                 "kept_centers_per_step": int(delta["centers"] / args.steps),
                 "targets_per_step": int(delta["targets"] / args.steps),
             },

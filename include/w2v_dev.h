@@ -154,6 +154,14 @@ int w2v_dev_reset_stats(w2v_dev* h);
  * as between the reference's OpenMP threads). -1 = every row atomic (the
  * default), 0 = none. Same fp32 rounding either way. */
 int w2v_dev_set_hot_rows(w2v_dev* h, int64_t hot_rows);
+/* The n hottest rows of the output layer (the NS target matrix, or the
+ * internal Huffman nodes nearest the root for HS) are additionally privatised
+ * per workgroup: their updates accumulate in LDS (ds_add_f32), reads see the
+ * HBM value plus the workgroup's pending delta, and each wavefront flushes the
+ * deltas with float atomics after every sentence. This takes the same-row
+ * atomic serialisation off the few rows every wavefront hits. -1 = as many as
+ * fit 40 KiB of LDS per workgroup (default), 0 = off. */
+int w2v_dev_set_private_rows(w2v_dev* h, int32_t n);
 
 /* Word2Vec::train_sentence_* take alpha from the caller (Word2Vec.h:83-84):
  * alpha > 0 makes every following epoch use it instead of the schedule of

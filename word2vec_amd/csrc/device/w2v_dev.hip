@@ -65,6 +65,7 @@ struct w2v_dev {
   int32_t d4 = 0;
   int nv = 1;                 // floats per lane per row (instantiated width >= ceil(d / 64))
   int64_t hot_rows = -1;      // rows updated with atomics: -1 = all, 0 = none
+  int32_t private_rows = -1;  // hottest output rows privatised in LDS: -1 = auto, 0 = off
   bool need_C = false, need_S = false;
   float* W = nullptr;
   float* C = nullptr;
@@ -503,19 +504,41 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     a.hot_s = (h->V - 1) - hot;  // the top `hot` internal nodes (the root is V-2)
   }
   a.strict = h->sched == W2V_SCHED_SEQUENTIAL ? 1 : 0;
+  // LDS privatisation of the output layer's hottest rows (the NS target matrix
+  // — C for skip-gram, W for CBOW — or the top of the Huffman tree for HS):
+  // as many rows as fit 40 KiB per workgroup (4 workgroups per CU), <= 64.
+  size_t lds_bytes = 0;
+  a.priv_M = nullptr;
+  a.priv_lo = 0;
+  a.priv_n = 0;
+  {
+    const int64_t row_bytes = (int64_t)h->nv * w2v::kWave * (int64_t)sizeof(float);
+    int64_t fit = (40 * 1024) / row_bytes;
+    if (fit > 64) fit = 64;
+    int64_t P = h->private_rows < 0 ? fit : (h->private_rows < fit ? h->private_rows : fit);
+    const bool hs = h->cfg.hs != 0;
+    const int64_t avail = hs ? h->V - 1 : h->V;
+    if (P > avail) P = avail;
+    if (P > 0) {
+      a.priv_M = hs ? h->S : (h->cfg.cbow ? h->W : h->C);
+      a.priv_lo = hs ? avail - P : 0;  // HS: the P internal nodes nearest the root (V-2)
+      a.priv_n = (int32_t)P;
+      lds_bytes = (size_t)(P * row_bytes);
+    }
+  }
   KernelFn fn = kernel_for(h);
   HIP_TRY(hipMemsetAsync(h->work, 0, sizeof(unsigned int), h->stream));
   dim3 grid(1), block(64);
   if (h->sched == W2V_SCHED_PARALLEL) {
     int per_cu = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds_bytes));
     if (per_cu < 1) per_cu = 1;
     const int64_t resident = (int64_t)per_cu * h->n_cu;
     const int64_t need = (count + 3) / 4;
     grid = dim3((unsigned)(need < resident ? need : resident));
     block = dim3(256);
   }
-  hipLaunchKernelGGL(fn, grid, block, 0, h->stream, a);
+  hipLaunchKernelGGL(fn, grid, block, lds_bytes, h->stream, a);
   HIP_TRY(hipGetLastError());
   return W2V_OK;
 }
@@ -579,6 +602,13 @@ int w2v_dev_reset_stats(w2v_dev* h) {
   if (set_device(h)) return W2V_ERR_HIP;
   HIP_TRY(hipMemsetAsync(h->counters + 1, 0, 7 * sizeof(unsigned long long), h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
+  return W2V_OK;
+}
+
+int w2v_dev_set_private_rows(w2v_dev* h, int32_t n) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (n < -1) return fail(W2V_ERR_ARG, "private_rows must be >= -1");
+  h->private_rows = n;
   return W2V_OK;
 }
 

@@ -81,6 +81,9 @@ struct TrainArgs {
   int64_t hot_wc;              // W / C rows [0, hot_wc) update with atomics
   int64_t hot_s;               // synapses1 rows [hot_s, V-1) update with atomics
   int32_t strict;              // 1: drain own atomics before re-reading (sequential schedule)
+  const float* priv_M;         // output matrix whose hottest rows are privatised in LDS (or null)
+  int64_t priv_lo;             // privatised rows [priv_lo, priv_lo + priv_n)
+  int32_t priv_n;
 };
 
 struct Counters {
@@ -212,15 +215,25 @@ __device__ __forceinline__ void add_to_row(float* M, int64_t row, bool hot, int6
 template <int NV, int MAXT, bool HSF>
 __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, int lane, int T, int row_l,
                                               int code_l, int t0, const float (&x)[NV], float (&g)[NV],
-                                              float alpha, int64_t hot_lo, int64_t hot_hi) {
+                                              float alpha, int64_t hot_lo, int64_t hot_hi, float* lds,
+                                              int64_t priv_lo, int64_t priv_n) {
   float r[MAXT][NV];
   int rows[MAXT];
-  bool hot[MAXT];
+  bool hot[MAXT], priv[MAXT];
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) {
     rows[t] = readlane_i(row_l, t0 + t);
-    hot[t] = rows[t] >= hot_lo && rows[t] < hot_hi;
-    if (t < T) load_row<NV>(M, rows[t], pitch, d, lane, hot[t], r[t]);
+    priv[t] = lds != nullptr && rows[t] >= priv_lo && rows[t] < priv_lo + priv_n;
+    hot[t] = !priv[t] && rows[t] >= hot_lo && rows[t] < hot_hi;
+    if (t < T) load_row<NV>(M, rows[t], pitch, d, lane, hot[t] || priv[t], r[t]);
+  }
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {  // privatised rows: global value + this workgroup's pending delta
+    if (t < T && priv[t]) {
+      const float* q = lds + (rows[t] - priv_lo) * (NV * kWave) + lane;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) r[t][v] += q[kWave * v];
+    }
   }
   float f[MAXT];
 #pragma unroll
@@ -252,7 +265,12 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
         g[v] += gt * r[t][v];  // grad uses the pre-update row (:244 / :266)
         delta[v] = gt * x[v];
       }
-      if (hot[t]) {
+      if (priv[t]) {  // ds_add_f32 into the workgroup's delta; flushed per sentence
+        float* q = lds + (rows[t] - priv_lo) * (NV * kWave) + lane;
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+          if (lane + kWave * v < d) atomicAdd(q + kWave * v, delta[v]);
+      } else if (hot[t]) {
         atomic_add_row<NV>(M, rows[t], pitch, d, lane, delta);
       } else {
 #pragma unroll
@@ -263,10 +281,32 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
   }
 }
 
+// Move this workgroup's pending deltas of the privatised rows into HBM (memory-
+// side float atomics), swapping each LDS word with 0 so concurrent adds by the
+// workgroup's other waves are neither lost nor flushed twice.
+template <int NV>
+__device__ __forceinline__ void flush_private(const TrainArgs& a, float* lds, int lane) {
+  if (lds == nullptr) return;
+  float* M = const_cast<float*>(a.priv_M);
+  for (int p = 0; p < a.priv_n; ++p) {
+    float* q = lds + p * (NV * kWave) + lane;
+    float* dst = M + (a.priv_lo + p) * a.pitch + lane;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      if (lane + kWave * v < a.dim) {
+        const float val = atomicExch(q + kWave * v, 0.0f);
+        if (val != 0.0f)
+          (void)__hip_atomic_fetch_add(dst + kWave * v, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
 // HS on the path of `word` (synapses1 rows).
 template <int NV, int MAXT>
 __device__ __forceinline__ void hs_word(const TrainArgs& a, int word, int lane, const float (&x)[NV],
-                                        float (&g)[NV], float alpha, Counters& cnt) {
+                                        float (&g)[NV], float alpha, Counters& cnt, float* lds) {
+  float* plds = (a.priv_M == a.S) ? lds : nullptr;
   const int64_t cb = a.coff[word];
   const int L = (int)(a.coff[word + 1] - cb);
   for (int c0 = 0; c0 < L; c0 += kWave) {
@@ -276,7 +316,7 @@ __device__ __forceinline__ void hs_word(const TrainArgs& a, int word, int lane, 
     for (int t0 = 0; t0 < rem; t0 += MAXT) {
       if (a.strict) drain_vmem();
       apply_targets<NV, MAXT, true>(a.S, a.pitch, a.dim, lane, min(MAXT, rem - t0), pt_l, cd_l, t0, x, g,
-                                    alpha, a.hot_s, INT64_MAX);
+                                    alpha, a.hot_s, INT64_MAX, plds, a.priv_lo, a.priv_n);
     }
     cnt.targets += (unsigned long long)rem;
   }
@@ -287,7 +327,9 @@ __device__ __forceinline__ void hs_word(const TrainArgs& a, int word, int lane, 
 // differ from it — the set semantics of Word2Vec.cpp:253-257) and applies it.
 template <int NV, int MAXT>
 __device__ __forceinline__ void ns_word(const TrainArgs& a, float* M, int word, int negw_l, int base, int lane,
-                                        const float (&x)[NV], float (&g)[NV], float alpha, Counters& cnt) {
+                                        const float (&x)[NV], float (&g)[NV], float alpha, Counters& cnt,
+                                        float* lds) {
+  float* plds = (a.priv_M == M) ? lds : nullptr;
   const int neg = a.negative;
   const int nk = __shfl(negw_l, (base + lane) & (kWave - 1));
   bool dup = (lane >= neg) || (nk == word);
@@ -310,7 +352,7 @@ __device__ __forceinline__ void ns_word(const TrainArgs& a, float* M, int word, 
   for (int t0 = 0; t0 < T; t0 += MAXT) {
     if (a.strict) drain_vmem();
     apply_targets<NV, MAXT, false>(M, a.pitch, a.dim, lane, min(MAXT, T - t0), tgt_l, code_l, t0, x, g, alpha,
-                                   0, a.hot_wc);
+                                   0, a.hot_wc, plds, a.priv_lo, a.priv_n);
   }
   cnt.targets += (unsigned long long)T;
 }
@@ -339,7 +381,7 @@ __device__ __forceinline__ int draw_negatives(const TrainArgs& a, uint32_t s, ui
 // Skip-gram center (Word2Vec.cpp:329-351) with its window [lo, hi).
 // ---------------------------------------------------------------------------
 template <int NV, int MAXT, bool HS, bool NS, bool REPLAY>
-__device__ __forceinline__ void sg_center(const TrainArgs& a, const int32_t* sent, int len, int i, int c, int rw,
+__device__ __forceinline__ void sg_center(const TrainArgs& a, float* lds, const int32_t* sent, int len, int i, int c, int rw,
                                           uint32_t s, float alpha, const uint32_t*& rp, Counters& cnt, int lane) {
   const int lo = max(0, i - a.window + rw), hi = min(len, i + a.window + 1 - rw);
   const int span = hi - lo;
@@ -360,7 +402,7 @@ __device__ __forceinline__ void sg_center(const TrainArgs& a, const int32_t* sen
   for (int j = lo; j < hi; ++j) {
     if (j == i) continue;
     const int w = readlane_i(ctx_l, j - lo);
-    if (HS) hs_word<NV, MAXT>(a, w, lane, x, g, alpha, cnt);
+    if (HS) hs_word<NV, MAXT>(a, w, lane, x, g, alpha, cnt, lds);
     if (NS) {
       const int gs = slot % G;
       if (gs == 0) {
@@ -368,7 +410,7 @@ __device__ __forceinline__ void sg_center(const TrainArgs& a, const int32_t* sen
         negw_l = draw_negatives<REPLAY>(a, s, (uint32_t)i, slot, nd, lane, rp);
         cnt.draws += (unsigned long long)nd;
       }
-      ns_word<NV, MAXT>(a, a.C, w, negw_l, gs * neg, lane, x, g, alpha, cnt);
+      ns_word<NV, MAXT>(a, a.C, w, negw_l, gs * neg, lane, x, g, alpha, cnt, lds);
     }
     ++slot;
   }
@@ -379,7 +421,7 @@ __device__ __forceinline__ void sg_center(const TrainArgs& a, const int32_t* sen
 // CBOW center (Word2Vec.cpp:286-315).
 // ---------------------------------------------------------------------------
 template <int NV, int MAXT, bool HS, bool NS, bool REPLAY>
-__device__ __forceinline__ void cbow_center(const TrainArgs& a, const int32_t* sent, int len, int i, int c, int rw,
+__device__ __forceinline__ void cbow_center(const TrainArgs& a, float* lds, const int32_t* sent, int len, int i, int c, int rw,
                                             uint32_t s, float alpha, const uint32_t*& rp, Counters& cnt, int lane) {
   const int lo = max(0, i - a.window + rw), hi = min(len, i + a.window + 1 - rw);
   const int n = hi - lo - 1;  // neu1_num, positional
@@ -441,12 +483,12 @@ __device__ __forceinline__ void cbow_center(const TrainArgs& a, const int32_t* s
 #pragma unroll
     for (int v = 0; v < NV; ++v) h[v] /= nf;
   }
-  if (HS) hs_word<NV, MAXT>(a, c, lane, h, g, alpha, cnt);
+  if (HS) hs_word<NV, MAXT>(a, c, lane, h, g, alpha, cnt, lds);
   if (NS) {
     const int nd = a.negative;
     const int negw_l = draw_negatives<REPLAY>(a, s, (uint32_t)i, 0, nd, lane, rp);
     cnt.draws += (unsigned long long)nd;
-    ns_word<NV, MAXT>(a, a.W, c, negw_l, 0, lane, h, g, alpha, cnt);
+    ns_word<NV, MAXT>(a, a.W, c, negw_l, 0, lane, h, g, alpha, cnt, lds);
   }
   if (a.cbow_mean) {
 #pragma unroll
@@ -459,12 +501,13 @@ __device__ __forceinline__ void cbow_center(const TrainArgs& a, const int32_t* s
 }
 
 template <int NV, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY>
-__device__ __forceinline__ void center(const TrainArgs& a, const int32_t* sent, int len, int i, int c, int rw,
-                                       uint32_t s, float alpha, const uint32_t*& rp, Counters& cnt, int lane) {
+__device__ __forceinline__ void center(const TrainArgs& a, float* lds, const int32_t* sent, int len, int i, int c,
+                                       int rw, uint32_t s, float alpha, const uint32_t*& rp, Counters& cnt,
+                                       int lane) {
   if (CBOW)
-    cbow_center<NV, MAXT, HS, NS, REPLAY>(a, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
+    cbow_center<NV, MAXT, HS, NS, REPLAY>(a, lds, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
   else
-    sg_center<NV, MAXT, HS, NS, REPLAY>(a, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
+    sg_center<NV, MAXT, HS, NS, REPLAY>(a, lds, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -472,7 +515,13 @@ __device__ __forceinline__ void center(const TrainArgs& a, const int32_t* sent, 
 // ---------------------------------------------------------------------------
 template <int NV, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY>
 __global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
+  extern __shared__ float w2v_lds[];
   const int lane = lane_id();
+  float* lds = a.priv_n > 0 ? w2v_lds : nullptr;
+  if (lds) {
+    for (int k = threadIdx.x; k < a.priv_n * NV * kWave; k += blockDim.x) lds[k] = 0.0f;
+    __syncthreads();
+  }
   Counters cnt;
   float alpha = a.init_alpha;
   bool first = true;
@@ -505,7 +554,7 @@ __global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
         if (a.keep[c] < u) continue;
         const int rw = (int)rp[0];
         ++rp;
-        center<NV, MAXT, CBOW, HS, NS, REPLAY>(a, sent, len, i, c, rw, (uint32_t)s, alpha, rp, cnt, lane);
+        center<NV, MAXT, CBOW, HS, NS, REPLAY>(a, lds, sent, len, i, c, rw, (uint32_t)s, alpha, rp, cnt, lane);
       }
     } else {
       for (int i0 = 0; i0 < len; i0 += kWave) {
@@ -522,13 +571,16 @@ __global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
           const int b = __builtin_ctzll(kept);
           kept &= kept - 1;
           const int c = readlane_i(c_l, b), rw = readlane_i(rw_l, b);
-          center<NV, MAXT, CBOW, HS, NS, REPLAY>(a, sent, len, i0 + b, c, rw, (uint32_t)s, alpha, rp, cnt, lane);
+          center<NV, MAXT, CBOW, HS, NS, REPLAY>(a, lds, sent, len, i0 + b, c, rw, (uint32_t)s, alpha, rp, cnt,
+                                                  lane);
         }
       }
     }
+    flush_private<NV>(a, lds, lane);
     if (lane == 0) atomicAdd(a.words, (unsigned long long)len);
     cnt.sentences += 1;
   }
+  flush_private<NV>(a, lds, lane);
   if (lane == 0) {
     atomicAdd(&a.stats[0], cnt.centers);
     atomicAdd(&a.stats[1], cnt.contexts);
@@ -555,9 +607,9 @@ __global__ __launch_bounds__(64) void apply_rows_kernel(float* M, int64_t pitch,
   for (int t = 0; t < n; ++t) {
     const int code = (int)codes[t];
     if (hs_form)
-      apply_targets<NV, 1, true>(M, pitch, d, lane, 1, t, code, 0, x, g, alpha, 0, 0);
+      apply_targets<NV, 1, true>(M, pitch, d, lane, 1, t, code, 0, x, g, alpha, 0, 0, nullptr, 0, 0);
     else
-      apply_targets<NV, 1, false>(M, pitch, d, lane, 1, t, code, 0, x, g, alpha, 0, 0);
+      apply_targets<NV, 1, false>(M, pitch, d, lane, 1, t, code, 0, x, g, alpha, 0, 0, nullptr, 0, 0);
   }
 #pragma unroll
   for (int v = 0; v < NV; ++v) {

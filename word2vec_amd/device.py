@@ -176,6 +176,10 @@ class DeviceTrainer:
         """Rows updated with atomics: -1 = all (default), 0 = none (plain Hogwild RMW), k = the k most frequent."""
         self._chk(self.lib.w2v_dev_set_hot_rows(self.h, int(hot_rows)), "w2v_dev_set_hot_rows")
 
+    def set_private_rows(self, n: int):
+        """Hottest output rows privatised per workgroup in LDS: -1 auto (default), 0 off."""
+        self._chk(self.lib.w2v_dev_set_private_rows(self.h, int(n)), "w2v_dev_set_private_rows")
+
     def set_fixed_alpha(self, alpha: float):
         self._chk(self.lib.w2v_dev_set_fixed_alpha(self.h, float(alpha)), "w2v_dev_set_fixed_alpha")
 
