@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -535,7 +536,12 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     if (per_cu < 1) per_cu = 1;
     const int64_t resident = (int64_t)per_cu * h->n_cu;
     const int64_t need = (count + 3) / 4;
-    grid = dim3((unsigned)(need < resident ? need : resident));
+    int64_t g = need < resident ? need : resident;
+    if (const char* cap = std::getenv("W2V_DEBUG_MAX_BLOCKS")) {  // diagnostics only
+      const int64_t c = std::atoll(cap);
+      if (c > 0 && c < g) g = c;
+    }
+    grid = dim3((unsigned)g);
     block = dim3(256);
   }
   hipLaunchKernelGGL(fn, grid, block, lds_bytes, h->stream, a);
