@@ -57,6 +57,8 @@ def parse():
                     help="rows updated with atomics (-1 all, 0 none = plain Hogwild RMW, k = k most frequent)")
     ap.add_argument("--private-rows", type=int, default=-1,
                     help="hottest output rows privatised per workgroup in LDS (-1 auto, 0 off)")
+    ap.add_argument("--own-model", action="store_true",
+                    help="N=1 only: let the library allocate the matrices instead of torch")
     ap.add_argument("--sync-every", type=int, default=0,
                     help="average the replicas every this many sentences of a shard (0 = once per step)")
     return ap.parse_args()
@@ -160,8 +162,16 @@ def main():
     if Cm is not None and mode["cbow"] and mode["hs"]:
         Cm[:, :d] = (torch.rand(V, d, generator=gW, device=dev) - 0.5) / d
     S = torch.zeros(max(V - 1, 1), pitch, dtype=torch.float32, device=dev) if mode["hs"] else None
-    tr.bind_model(W.data_ptr(), Cm.data_ptr() if Cm is not None else None,
-                  S.data_ptr() if S is not None else None, pitch)
+    if args.own_model and world == 1:
+        Wn = W[:, :d].cpu().numpy()
+        Cn = Cm[:, :d].cpu().numpy() if Cm is not None else None
+        Sn = S[:, :d].cpu().numpy() if S is not None else None
+        tr.upload_model(Wn, Cn, Sn)
+        del Wn, Cn, Sn
+        W = Cm = S = None
+    else:
+        tr.bind_model(W.data_ptr(), Cm.data_ptr() if Cm is not None else None,
+                      S.data_ptr() if S is not None else None, pitch)
     tr.upload_corpus(ids_h, soff_h, n_tok * world)  # alpha follows the global raw-token total
     tr.set_rng(N.W2V_RNG_PHILOX, (args.seed << 32) | (rank + 1))
     tr.set_schedule(N.W2V_SCHED_PARALLEL)
@@ -172,6 +182,8 @@ def main():
     log(f"[bench] resident in HBM ({time.time() - t0:.1f}s)")
 
     mats = [m for m in (W, Cm, S) if m is not None]
+    if not mats:
+        assert world == 1
     replicas = ReplicaGroup(mats, world)
     rounds = n_rounds(n_sent * world, world, args.sync_every)
     order_dev = torch.arange(n_sent, dtype=torch.int64, device=dev)  # this rank's shard, in order

@@ -313,20 +313,30 @@ int w2v_dev_upload_table(w2v_dev* h, const uint32_t* table, int64_t n) {
   return W2V_OK;
 }
 
+// Model allocation flavour (experiments): W2V_MATRIX_ALLOC=uncached|finegrained.
+static hipError_t model_malloc(float** p, size_t bytes) {
+  const char* mode = std::getenv("W2V_MATRIX_ALLOC");
+  if (mode && !std::strcmp(mode, "uncached"))
+    return hipExtMallocWithFlags(reinterpret_cast<void**>(p), bytes, hipDeviceMallocUncached);
+  if (mode && !std::strcmp(mode, "finegrained"))
+    return hipExtMallocWithFlags(reinterpret_cast<void**>(p), bytes, hipDeviceMallocFinegrained);
+  return hipMalloc(p, bytes);
+}
+
 static int ensure_model(w2v_dev* h) {
   if (h->V < 1) return fail(W2V_ERR_STATE, "upload the vocab before the model");
   const size_t rows_bytes = (size_t)h->V * h->pitch * sizeof(float);
   if (!h->W) {
-    HIP_TRY(hipMalloc(&h->W, rows_bytes));
+    HIP_TRY(model_malloc(&h->W, rows_bytes));
     HIP_TRY(hipMemset(h->W, 0, rows_bytes));
   }
   if (h->need_C && !h->C) {
-    HIP_TRY(hipMalloc(&h->C, rows_bytes));
+    HIP_TRY(model_malloc(&h->C, rows_bytes));
     HIP_TRY(hipMemset(h->C, 0, rows_bytes));
   }
   if (h->need_S && !h->S) {
     const size_t sb = (size_t)(h->V > 1 ? h->V - 1 : 1) * h->pitch * sizeof(float);
-    HIP_TRY(hipMalloc(&h->S, sb));
+    HIP_TRY(model_malloc(&h->S, sb));
     HIP_TRY(hipMemset(h->S, 0, sb));
   }
   return W2V_OK;
@@ -505,6 +515,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     a.hot_s = (h->V - 1) - hot;  // the top `hot` internal nodes (the root is V-2)
   }
   a.strict = h->sched == W2V_SCHED_SEQUENTIAL ? 1 : 0;
+  a.fresh_all = std::getenv("W2V_FRESH_LOADS") ? 1 : 0;  // experiment: every row gather bypasses L1
   // LDS privatisation of the output layer's hottest rows (the NS target matrix
   // — C for skip-gram, W for CBOW — or the top of the Huffman tree for HS):
   // as many rows as fit 40 KiB per workgroup (4 workgroups per CU), <= 64.

@@ -84,6 +84,7 @@ struct TrainArgs {
   const float* priv_M;         // output matrix whose hottest rows are privatised in LDS (or null)
   int64_t priv_lo;             // privatised rows [priv_lo, priv_lo + priv_n)
   int32_t priv_n;
+  int32_t fresh_all;           // every row gather uses L1-bypassing loads
 };
 
 struct Counters {
@@ -216,7 +217,7 @@ template <int NV, int MAXT, bool HSF>
 __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, int lane, int T, int row_l,
                                               int code_l, int t0, const float (&x)[NV], float (&g)[NV],
                                               float alpha, int64_t hot_lo, int64_t hot_hi, float* lds,
-                                              int64_t priv_lo, int64_t priv_n) {
+                                              int64_t priv_lo, int64_t priv_n, bool fresh = false) {
   float r[MAXT][NV];
   int rows[MAXT];
   bool hot[MAXT], priv[MAXT];
@@ -225,7 +226,7 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
     rows[t] = readlane_i(row_l, t0 + t);
     priv[t] = lds != nullptr && rows[t] >= priv_lo && rows[t] < priv_lo + priv_n;
     hot[t] = !priv[t] && rows[t] >= hot_lo && rows[t] < hot_hi;
-    if (t < T) load_row<NV>(M, rows[t], pitch, d, lane, hot[t] || priv[t], r[t]);
+    if (t < T) load_row<NV>(M, rows[t], pitch, d, lane, hot[t] || priv[t] || fresh, r[t]);
   }
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) {  // privatised rows: global value + this workgroup's pending delta
@@ -316,7 +317,7 @@ __device__ __forceinline__ void hs_word(const TrainArgs& a, int word, int lane, 
     for (int t0 = 0; t0 < rem; t0 += MAXT) {
       if (a.strict) drain_vmem();
       apply_targets<NV, MAXT, true>(a.S, a.pitch, a.dim, lane, min(MAXT, rem - t0), pt_l, cd_l, t0, x, g,
-                                    alpha, a.hot_s, INT64_MAX, plds, a.priv_lo, a.priv_n);
+                                    alpha, a.hot_s, INT64_MAX, plds, a.priv_lo, a.priv_n, a.fresh_all != 0);
     }
     cnt.targets += (unsigned long long)rem;
   }
@@ -352,7 +353,7 @@ __device__ __forceinline__ void ns_word(const TrainArgs& a, float* M, int word, 
   for (int t0 = 0; t0 < T; t0 += MAXT) {
     if (a.strict) drain_vmem();
     apply_targets<NV, MAXT, false>(M, a.pitch, a.dim, lane, min(MAXT, T - t0), tgt_l, code_l, t0, x, g, alpha,
-                                   0, a.hot_wc, plds, a.priv_lo, a.priv_n);
+                                   0, a.hot_wc, plds, a.priv_lo, a.priv_n, a.fresh_all != 0);
   }
   cnt.targets += (unsigned long long)T;
 }
