@@ -173,11 +173,17 @@ __device__ __forceinline__ void load_row(const float* M, int64_t row, int64_t pi
 
 template <int NV>
 __device__ __forceinline__ void store_row(float* M, int64_t row, int64_t pitch, int d, int lane,
-                                          const float (&r)[NV]) {
+                                          const float (&r)[NV], bool wt = false) {
   float* p = M + row * pitch + lane;
+  if (wt) {  // global_store_dword sc1: write through and drop the line from this XCD's L2
 #pragma unroll
-  for (int v = 0; v < NV; ++v)
-    if (lane + kWave * v < d) p[kWave * v] = r[v];
+    for (int v = 0; v < NV; ++v)
+      if (lane + kWave * v < d) __hip_atomic_store(p + kWave * v, r[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+      if (lane + kWave * v < d) p[kWave * v] = r[v];
+  }
 }
 
 // row += delta, memory-side (no-return global_atomic_add_f32, 256 contiguous B per instruction)
@@ -194,15 +200,15 @@ __device__ __forceinline__ void atomic_add_row(float* M, int64_t row, int64_t pi
 // M[row] += delta: atomically for hot rows; else read-modify-write (Hogwild).
 template <int NV>
 __device__ __forceinline__ void add_to_row(float* M, int64_t row, bool hot, int64_t pitch, int d, int lane,
-                                           const float (&delta)[NV]) {
+                                           const float (&delta)[NV], bool fresh = false) {
   if (hot) {
     atomic_add_row<NV>(M, row, pitch, d, lane, delta);
   } else {
     float cur[NV];
-    load_row<NV>(M, row, pitch, d, lane, false, cur);
+    load_row<NV>(M, row, pitch, d, lane, fresh, cur);
 #pragma unroll
     for (int v = 0; v < NV; ++v) cur[v] += delta[v];
-    store_row<NV>(M, row, pitch, d, lane, cur);
+    store_row<NV>(M, row, pitch, d, lane, cur, fresh);
   }
 }
 
@@ -276,7 +282,7 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
       } else {
 #pragma unroll
         for (int v = 0; v < NV; ++v) r[t][v] += delta[v];
-        store_row<NV>(M, rows[t], pitch, d, lane, r[t]);
+        store_row<NV>(M, rows[t], pitch, d, lane, r[t], fresh);
       }
     }
   }
@@ -389,7 +395,7 @@ __device__ __forceinline__ void sg_center(const TrainArgs& a, float* lds, const 
   const bool hot_c = c < a.hot_wc;
   float x[NV], g[NV];
   if (a.strict) drain_vmem();
-  load_row<NV>(a.W, c, a.pitch, a.dim, lane, hot_c, x);
+  load_row<NV>(a.W, c, a.pitch, a.dim, lane, hot_c || a.fresh_all, x);
 #pragma unroll
   for (int v = 0; v < NV; ++v) g[v] = 0.f;
   const int ctx_l = (lane < span) ? sent[lo + lane] : 0;
@@ -415,7 +421,7 @@ __device__ __forceinline__ void sg_center(const TrainArgs& a, float* lds, const 
     }
     ++slot;
   }
-  add_to_row<NV>(a.W, c, hot_c, a.pitch, a.dim, lane, g);  // W.row(center) += neu1_grad (:351)
+  add_to_row<NV>(a.W, c, hot_c, a.pitch, a.dim, lane, g, a.fresh_all != 0);  // W.row(center) += neu1_grad (:351)
 }
 
 // ---------------------------------------------------------------------------
@@ -470,7 +476,7 @@ __device__ __forceinline__ void cbow_center(const TrainArgs& a, float* lds, cons
     for (int t = 0; t < MAXT; ++t)
       if (r0 + t < U) {
         const int row = readlane_i(sid, r0 + t);
-        load_row<NV>(a.C, row, a.pitch, a.dim, lane, row < a.hot_wc, rr[t]);
+        load_row<NV>(a.C, row, a.pitch, a.dim, lane, row < a.hot_wc || a.fresh_all, rr[t]);
       }
 #pragma unroll
     for (int t = 0; t < MAXT; ++t)
@@ -497,7 +503,7 @@ __device__ __forceinline__ void cbow_center(const TrainArgs& a, float* lds, cons
   }
   for (int r = 0; r < U; ++r) {  // C.row(id) += neu1_grad for every unique id (:315)
     const int row = readlane_i(sid, r);
-    add_to_row<NV>(a.C, row, row < a.hot_wc, a.pitch, a.dim, lane, g);
+    add_to_row<NV>(a.C, row, row < a.hot_wc, a.pitch, a.dim, lane, g, a.fresh_all != 0);
   }
 }
 
