@@ -57,6 +57,8 @@ def parse():
                     help="rows updated with atomics (-1 all, 0 none = plain Hogwild RMW, k = k most frequent)")
     ap.add_argument("--private-rows", type=int, default=-1,
                     help="hottest output rows privatised per workgroup in LDS (-1 auto, 0 off)")
+    ap.add_argument("--max-waves", type=int, default=-1,
+                    help="wavefronts in flight (-1: 1024 for hs, all otherwise; 0 = all)")
     ap.add_argument("--own-model", action="store_true",
                     help="N=1 only: let the library allocate the matrices instead of torch")
     ap.add_argument("--sync-every", type=int, default=0,
@@ -177,6 +179,7 @@ def main():
     tr.set_schedule(N.W2V_SCHED_PARALLEL)
     tr.set_hot_rows(args.hot_rows)
     tr.set_private_rows(args.private_rows)
+    tr.set_max_waves(args.max_waves if args.max_waves >= 0 else (1024 if mode["hs"] else 0))
     tr.set_progress(0)
     torch.cuda.synchronize()
     log(f"[bench] resident in HBM ({time.time() - t0:.1f}s)")
@@ -272,6 +275,7 @@ def main():
                                 f"average x{rounds} per step" if world > 1 else "dp1"),
                 "hot_rows": args.hot_rows,
                 "private_rows": args.private_rows,
+                "max_waves": args.max_waves,
                 "kept_centers_per_step": int(delta["centers"] / args.steps),
                 "targets_per_step": int(delta["targets"] / args.steps),
             },

@@ -99,6 +99,7 @@ class Word2Vec {
                              // single-threaded up to fp32 summation order)
   int64_t hot_rows = -1;     // rows updated with device atomics (w2v_dev_set_hot_rows): -1 all
   int private_rows = -1;     // hottest output rows privatised in LDS (w2v_dev_set_private_rows)
+  int64_t max_waves = -1;    // wavefronts in flight (w2v_dev_set_max_waves); -1 = 1024 for hs, else all
   bool verbose = true;       // progress line per epoch (the reference prints one
                              // every 100 sentences, Word2Vec.cpp:382-386)
   // Train on a corpus that is already token ids (no strings): ids index

@@ -158,10 +158,15 @@ int w2v_dev_set_hot_rows(w2v_dev* h, int64_t hot_rows);
  * internal Huffman nodes nearest the root for HS) are additionally privatised
  * per workgroup: their updates accumulate in LDS (ds_add_f32), reads see the
  * HBM value plus the workgroup's pending delta, and each wavefront flushes the
- * deltas with float atomics after every sentence. This takes the same-row
- * atomic serialisation off the few rows every wavefront hits. -1 = as many as
- * fit 40 KiB of LDS per workgroup (default), 0 = off. */
+ * deltas with float atomics after every center (staleness bounded by one
+ * center). This takes the same-row atomic serialisation off the few rows
+ * every wavefront hits. -1 = as many as fit 40 KiB of LDS per workgroup, at
+ * most 32 (default); 0 = off. Not used by the sequential schedule. */
 int w2v_dev_set_private_rows(w2v_dev* h, int32_t n);
+/* Cap on wavefronts in flight in the parallel schedule (0 = as many as fit).
+ * Hogwild staleness grows with it: every hierarchical-softmax call updates
+ * the Huffman root, so HS needs a cap (~1024) to stay stable. */
+int w2v_dev_set_max_waves(w2v_dev* h, int64_t n);
 
 /* Word2Vec::train_sentence_* take alpha from the caller (Word2Vec.h:83-84):
  * alpha > 0 makes every following epoch use it instead of the schedule of

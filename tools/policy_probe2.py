@@ -26,9 +26,5 @@ def run(mode, hot, priv, env):
     print(f"{mode} hot={hot} priv={priv} {env}: analogy {analogy_accuracy(words, E, qs)['accuracy']:.2f} "
           f"sim {similarity_score(words, E, pairs)['spearman']:.2f} (oracle {ref[0]:.2f} {ref[1]:.2f})", flush=True)
 for mode in MODES:
-    run(mode, 0, 0, {"W2V_FRESH_LOADS": "1"})
-    run(mode, -1, 0, {})
-for mode in ("sg_hs", "cbow_hs"):
-    for cap in (16, 64, 256):
-        run(mode, -1, 0, {"W2V_DEBUG_MAX_BLOCKS": str(cap)})
-        run(mode, 0, 0, {"W2V_DEBUG_MAX_BLOCKS": str(cap), "W2V_FRESH_LOADS": "1"})
+    for hot, priv in [(-1, -1), (10000, -1), (-1, 0)]:
+        run(mode, hot, priv, {})

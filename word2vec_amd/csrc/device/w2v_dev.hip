@@ -67,6 +67,7 @@ struct w2v_dev {
   int nv = 1;                 // floats per lane per row (instantiated width >= ceil(d / 64))
   int64_t hot_rows = -1;      // rows updated with atomics: -1 = all, 0 = none
   int32_t private_rows = -1;  // hottest output rows privatised in LDS: -1 = auto, 0 = off
+  int64_t max_waves = 0;      // cap on concurrently scheduled wavefronts (0 = as many as fit)
   bool need_C = false, need_S = false;
   float* W = nullptr;
   float* C = nullptr;
@@ -525,17 +526,18 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   a.priv_n = 0;
   {
     const int64_t row_bytes = (int64_t)h->nv * w2v::kWave * (int64_t)sizeof(float);
-    int64_t fit = (40 * 1024) / row_bytes;
-    if (fit > 64) fit = 64;
+    int64_t fit = (40 * 1024 - 16) / row_bytes;
+    if (fit > 32) fit = 32;
     int64_t P = h->private_rows < 0 ? fit : (h->private_rows < fit ? h->private_rows : fit);
     const bool hs = h->cfg.hs != 0;
     const int64_t avail = hs ? h->V - 1 : h->V;
     if (P > avail) P = avail;
+    if (h->sched == W2V_SCHED_SEQUENTIAL) P = 0;  // the reference-exact schedule keeps per-update rounding
     if (P > 0) {
       a.priv_M = hs ? h->S : (h->cfg.cbow ? h->W : h->C);
       a.priv_lo = hs ? avail - P : 0;  // HS: the P internal nodes nearest the root (V-2)
       a.priv_n = (int32_t)P;
-      lds_bytes = (size_t)(P * row_bytes);
+      lds_bytes = (size_t)(P * row_bytes) + 16;  // + the dirty mask
     }
   }
   KernelFn fn = kernel_for(h);
@@ -548,6 +550,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     const int64_t resident = (int64_t)per_cu * h->n_cu;
     const int64_t need = (count + 3) / 4;
     int64_t g = need < resident ? need : resident;
+    if (h->max_waves > 0 && (h->max_waves + 3) / 4 < g) g = (h->max_waves + 3) / 4;
     if (const char* cap = std::getenv("W2V_DEBUG_MAX_BLOCKS")) {  // diagnostics only
       const int64_t c = std::atoll(cap);
       if (c > 0 && c < g) g = c;
@@ -619,6 +622,13 @@ int w2v_dev_reset_stats(w2v_dev* h) {
   if (set_device(h)) return W2V_ERR_HIP;
   HIP_TRY(hipMemsetAsync(h->counters + 1, 0, 7 * sizeof(unsigned long long), h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
+  return W2V_OK;
+}
+
+int w2v_dev_set_max_waves(w2v_dev* h, int64_t n) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (n < 0) return fail(W2V_ERR_ARG, "max_waves must be >= 0");
+  h->max_waves = n;
   return W2V_OK;
 }
 

@@ -272,11 +272,14 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
         g[v] += gt * r[t][v];  // grad uses the pre-update row (:244 / :266)
         delta[v] = gt * x[v];
       }
-      if (priv[t]) {  // ds_add_f32 into the workgroup's delta; flushed per sentence
-        float* q = lds + (rows[t] - priv_lo) * (NV * kWave) + lane;
+      if (priv[t]) {  // ds_add_f32 into the workgroup's delta; flushed after the center
+        const int64_t pr = rows[t] - priv_lo;
+        float* q = lds + pr * (NV * kWave) + lane;
 #pragma unroll
         for (int v = 0; v < NV; ++v)
           if (lane + kWave * v < d) atomicAdd(q + kWave * v, delta[v]);
+        if (lane == 0)  // after the adds (a wave's LDS ops are ordered): mark the row dirty
+          atomicOr(reinterpret_cast<unsigned long long*>(lds + priv_n * (NV * kWave)), 1ull << pr);
       } else if (hot[t]) {
         atomic_add_row<NV>(M, rows[t], pitch, d, lane, delta);
       } else {
@@ -288,14 +291,23 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
   }
 }
 
-// Move this workgroup's pending deltas of the privatised rows into HBM (memory-
-// side float atomics), swapping each LDS word with 0 so concurrent adds by the
-// workgroup's other waves are neither lost nor flushed twice.
+// Move the workgroup's pending deltas of the dirty privatised rows into HBM
+// (memory-side float atomics). The dirty mask and every delta word are taken
+// with atomic swaps, so an add racing the flush from another wave of the
+// workgroup is neither lost nor flushed twice (its dirty bit is set after its
+// adds and survives until the next flush).
 template <int NV>
 __device__ __forceinline__ void flush_private(const TrainArgs& a, float* lds, int lane) {
   if (lds == nullptr) return;
+  unsigned long long* dirty = reinterpret_cast<unsigned long long*>(lds + a.priv_n * (NV * kWave));
+  unsigned long long m = 0;
+  if (lane == 0) m = atomicExch(dirty, 0ull);
+  m = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(m >> 32)) << 32) |
+      (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)m);
   float* M = const_cast<float*>(a.priv_M);
-  for (int p = 0; p < a.priv_n; ++p) {
+  while (m) {
+    const int p = __builtin_ctzll(m);
+    m &= m - 1;
     float* q = lds + p * (NV * kWave) + lane;
     float* dst = M + (a.priv_lo + p) * a.pitch + lane;
 #pragma unroll
@@ -515,6 +527,7 @@ __device__ __forceinline__ void center(const TrainArgs& a, float* lds, const int
     cbow_center<NV, MAXT, HS, NS, REPLAY>(a, lds, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
   else
     sg_center<NV, MAXT, HS, NS, REPLAY>(a, lds, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
+  flush_private<NV>(a, lds, lane);  // bounded staleness: pending deltas live for one center
 }
 
 // ---------------------------------------------------------------------------
@@ -526,7 +539,7 @@ __global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
   const int lane = lane_id();
   float* lds = a.priv_n > 0 ? w2v_lds : nullptr;
   if (lds) {
-    for (int k = threadIdx.x; k < a.priv_n * NV * kWave; k += blockDim.x) lds[k] = 0.0f;
+    for (int k = threadIdx.x; k < a.priv_n * NV * kWave + 2; k += blockDim.x) lds[k] = 0.0f;  // deltas + dirty mask
     __syncthreads();
   }
   Counters cnt;
@@ -583,7 +596,6 @@ __global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
         }
       }
     }
-    flush_private<NV>(a, lds, lane);
     if (lane == 0) atomicAdd(a.words, (unsigned long long)len);
     cnt.sentences += 1;
   }

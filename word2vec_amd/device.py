@@ -180,6 +180,10 @@ class DeviceTrainer:
         """Hottest output rows privatised per workgroup in LDS: -1 auto (default), 0 off."""
         self._chk(self.lib.w2v_dev_set_private_rows(self.h, int(n)), "w2v_dev_set_private_rows")
 
+    def set_max_waves(self, n: int):
+        """Cap on wavefronts in flight (0 = as many as fit)."""
+        self._chk(self.lib.w2v_dev_set_max_waves(self.h, int(n)), "w2v_dev_set_max_waves")
+
     def set_fixed_alpha(self, alpha: float):
         self._chk(self.lib.w2v_dev_set_fixed_alpha(self.h, float(alpha)), "w2v_dev_set_fixed_alpha")
 
