@@ -12,7 +12,7 @@ from word2vec_amd.model import Word2Vec
 sents, qs, pairs = planted_corpus(**CORPUS)
 GOLD = json.loads((ROOT / "tests" / "golden" / "quality_oracle.json").read_text())
 def run(mode, hot, priv, env):
-    for k in ("W2V_FRESH_LOADS", "W2V_DEBUG_MAX_BLOCKS"):
+    for k in ("W2V_FRESH_LOADS", "W2V_DEBUG_MAX_BLOCKS", "W2V_FLUSH_EVERY"):
         os.environ.pop(k, None)
     os.environ.update(env)
     m = MODES[mode]
@@ -25,6 +25,6 @@ def run(mode, hot, priv, env):
     E = w.matrix(1 if mode == "cbow_hs" else 0)
     print(f"{mode} hot={hot} priv={priv} {env}: analogy {analogy_accuracy(words, E, qs)['accuracy']:.2f} "
           f"sim {similarity_score(words, E, pairs)['spearman']:.2f} (oracle {ref[0]:.2f} {ref[1]:.2f})", flush=True)
-for mode in MODES:
-    for hot, priv in [(-1, -1), (10000, -1), (-1, 0)]:
-        run(mode, hot, priv, {})
+for F in (1, 2, 4, 8, 16):
+    for mode in ("sg_ns", "cbow_hs"):
+        run(mode, -1, -1, {"W2V_FLUSH_EVERY": str(F)})

@@ -517,6 +517,8 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   }
   a.strict = h->sched == W2V_SCHED_SEQUENTIAL ? 1 : 0;
   a.fresh_all = std::getenv("W2V_FRESH_LOADS") ? 1 : 0;  // experiment: every row gather bypasses L1
+  a.flush_every = 1;
+  if (const char* f = std::getenv("W2V_FLUSH_EVERY")) a.flush_every = std::atoi(f) > 0 ? std::atoi(f) : 1;
   // LDS privatisation of the output layer's hottest rows (the NS target matrix
   // — C for skip-gram, W for CBOW — or the top of the Huffman tree for HS):
   // as many rows as fit 40 KiB per workgroup (4 workgroups per CU), <= 64.

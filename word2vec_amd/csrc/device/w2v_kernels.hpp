@@ -85,6 +85,7 @@ struct TrainArgs {
   int64_t priv_lo;             // privatised rows [priv_lo, priv_lo + priv_n)
   int32_t priv_n;
   int32_t fresh_all;           // every row gather uses L1-bypassing loads
+  int32_t flush_every;         // a wavefront flushes the privatised deltas every this many centers
 };
 
 struct Counters {
@@ -522,12 +523,15 @@ __device__ __forceinline__ void cbow_center(const TrainArgs& a, float* lds, cons
 template <int NV, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY>
 __device__ __forceinline__ void center(const TrainArgs& a, float* lds, const int32_t* sent, int len, int i, int c,
                                        int rw, uint32_t s, float alpha, const uint32_t*& rp, Counters& cnt,
-                                       int lane) {
+                                       int lane, int& since_flush) {
   if (CBOW)
     cbow_center<NV, MAXT, HS, NS, REPLAY>(a, lds, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
   else
     sg_center<NV, MAXT, HS, NS, REPLAY>(a, lds, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
-  flush_private<NV>(a, lds, lane);  // bounded staleness: pending deltas live for one center
+  if (++since_flush >= a.flush_every) {  // bounded staleness: deltas live for flush_every centers
+    flush_private<NV>(a, lds, lane);
+    since_flush = 0;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -543,6 +547,7 @@ __global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
     __syncthreads();
   }
   Counters cnt;
+  int since_flush = 0;
   float alpha = a.init_alpha;
   bool first = true;
   const uint32_t wmax = (uint32_t)(a.window < 1 ? 1 : a.window);
@@ -574,7 +579,8 @@ __global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
         if (a.keep[c] < u) continue;
         const int rw = (int)rp[0];
         ++rp;
-        center<NV, MAXT, CBOW, HS, NS, REPLAY>(a, lds, sent, len, i, c, rw, (uint32_t)s, alpha, rp, cnt, lane);
+        center<NV, MAXT, CBOW, HS, NS, REPLAY>(a, lds, sent, len, i, c, rw, (uint32_t)s, alpha, rp, cnt, lane,
+                                                since_flush);
       }
     } else {
       for (int i0 = 0; i0 < len; i0 += kWave) {
@@ -592,7 +598,7 @@ __global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
           kept &= kept - 1;
           const int c = readlane_i(c_l, b), rw = readlane_i(rw_l, b);
           center<NV, MAXT, CBOW, HS, NS, REPLAY>(a, lds, sent, len, i0 + b, c, rw, (uint32_t)s, alpha, rp, cnt,
-                                                  lane);
+                                                  lane, since_flush);
         }
       }
     }
