@@ -62,3 +62,46 @@ def planted_corpus(n_sent=3000, sent_len=200, rows=30, cols=4, topic_per_row=6, 
                     if (a, b) < (c, d) and rng.random() < 0.15:
                         pairs.append((ent[a][b], ent[c][d], float((a == c) + (b == d))))
     return sents, questions, pairs
+
+
+def planted_zipf_corpus(n_tokens=10_000_000, sent_len=1000, filler=100_000, rows=50, cols=4, topic_per_row=8,
+                        role_per_col=8, planted_frac=0.25, seed=0):
+    """Text8-like statistics: Zipf(s=1) filler over `filler` word types (the
+    function words are the hottest rows), 1000-token sentences, and the planted
+    relations of planted_corpus() embedded at mid frequency: in each sentence a
+    fraction `planted_frac` of positions carries the sentence's (row, col)
+    entity / topic / role words, spread through the filler."""
+    rng = np.random.default_rng(seed)
+    n_sent = n_tokens // sent_len
+    ent = np.array([[f"e{i}_{j}" for j in range(cols)] for i in range(rows)])
+    topic = np.array([[f"t{i}_{k}" for k in range(topic_per_row)] for i in range(rows)])
+    role = np.array([[f"r{j}_{k}" for k in range(role_per_col)] for j in range(cols)])
+    p = 1.0 / np.arange(1, filler + 1)
+    cdf = np.cumsum(p)
+    cdf /= cdf[-1]
+    fill_ids = np.searchsorted(cdf, rng.random(n_sent * sent_len), side="right").clip(0, filler - 1)
+    sents = []
+    for s in range(n_sent):
+        toks = [f"f{x}" for x in fill_ids[s * sent_len:(s + 1) * sent_len]]
+        i, j = rng.integers(rows), rng.integers(cols)
+        pos = np.flatnonzero(rng.random(sent_len) < planted_frac)
+        kind = rng.random(pos.size)
+        for q, kk in zip(pos, kind):
+            if kk < 0.34:
+                toks[q] = ent[i, j] if rng.random() > 0.25 else (ent[i, rng.integers(cols)] if rng.random() < 0.5
+                                                                  else ent[rng.integers(rows), j])
+            elif kk < 0.67:
+                toks[q] = topic[i, rng.integers(topic_per_row)]
+            else:
+                toks[q] = role[j, rng.integers(role_per_col)]
+        sents.append(toks)
+    questions = [(ent[i, l], ent[i, j], ent[k, l], ent[k, j]) for i in range(rows) for k in range(rows) if i != k
+                 for j in range(cols) for l in range(cols) if j != l]
+    pairs = []
+    for a in range(rows):
+        for b in range(cols):
+            for c in range(rows):
+                for d in range(cols):
+                    if (a, b) < (c, d) and rng.random() < 0.05:
+                        pairs.append((ent[a, b], ent[c, d], float((a == c) + (b == d))))
+    return sents, questions, pairs
