@@ -156,14 +156,15 @@ def main():
     tr.set_stream(stream.cuda_stream)
     tr.upload_vocab(keep, bounds, codes, points, coff)
     pitch = (d + 31) // 32 * 32
+    vrows = -(-V // 4096) * 4096 if os.environ.get("W2V_DEV_LIB") else V  # room for the scramble experiment
     gW = torch.Generator(device=dev)
     gW.manual_seed(args.seed)  # identical initial replicas on every rank
-    W = torch.zeros(V, pitch, dtype=torch.float32, device=dev)
-    W[:, :d] = (torch.rand(V, d, generator=gW, device=dev) - 0.5) / d
-    Cm = torch.zeros(V, pitch, dtype=torch.float32, device=dev) if (neg > 0 or mode["cbow"]) else None
+    W = torch.zeros(vrows, pitch, dtype=torch.float32, device=dev)
+    W[:V, :d] = (torch.rand(V, d, generator=gW, device=dev) - 0.5) / d
+    Cm = torch.zeros(vrows, pitch, dtype=torch.float32, device=dev) if (neg > 0 or mode["cbow"]) else None
     if Cm is not None and mode["cbow"] and mode["hs"]:
-        Cm[:, :d] = (torch.rand(V, d, generator=gW, device=dev) - 0.5) / d
-    S = torch.zeros(max(V - 1, 1), pitch, dtype=torch.float32, device=dev) if mode["hs"] else None
+        Cm[:V, :d] = (torch.rand(V, d, generator=gW, device=dev) - 0.5) / d
+    S = torch.zeros(max(vrows, 1), pitch, dtype=torch.float32, device=dev) if mode["hs"] else None
     if args.own_model and world == 1:
         Wn = W[:, :d].cpu().numpy()
         Cn = Cm[:, :d].cpu().numpy() if Cm is not None else None

@@ -98,7 +98,7 @@ def load_dev_lib(path: os.PathLike | str | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else DEV_LIB
+    p = Path(path) if path else Path(os.environ.get("W2V_DEV_LIB", DEV_LIB))
     if not p.exists():
         raise RuntimeError(
             f"word2vec_amd: HIP library {p} is missing; build it with "

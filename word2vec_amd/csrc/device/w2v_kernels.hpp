@@ -156,10 +156,15 @@ __device__ __forceinline__ uint32_t philox_table_pos(const TrainArgs& a, uint32_
 // ---------------------------------------------------------------------------
 // Row I/O: a row is NV floats per lane, element lane + 64 v (v < NV).
 // ---------------------------------------------------------------------------
+#ifdef W2V_SCRAMBLE  // experiment build: spread consecutive rows 1031 slots apart inside 4096-row blocks
+__device__ __forceinline__ int64_t phys_row(int64_t r) { return (r & ~4095LL) | (((r & 4095) * 1031) & 4095); }
+#else
+__device__ __forceinline__ int64_t phys_row(int64_t r) { return r; }
+#endif
 template <int NV>
 __device__ __forceinline__ void load_row(const float* M, int64_t row, int64_t pitch, int d, int lane,
                                          bool fresh, float (&r)[NV]) {
-  const float* p = M + row * pitch + lane;
+  const float* p = M + phys_row(row) * pitch + lane;
   if (fresh) {  // agent-scope relaxed loads: global_load_dword sc1, bypass the CU's L1
 #pragma unroll
     for (int v = 0; v < NV; ++v)
@@ -175,7 +180,7 @@ __device__ __forceinline__ void load_row(const float* M, int64_t row, int64_t pi
 template <int NV>
 __device__ __forceinline__ void store_row(float* M, int64_t row, int64_t pitch, int d, int lane,
                                           const float (&r)[NV], bool wt = false) {
-  float* p = M + row * pitch + lane;
+  float* p = M + phys_row(row) * pitch + lane;
   if (wt) {  // global_store_dword sc1: write through and drop the line from this XCD's L2
 #pragma unroll
     for (int v = 0; v < NV; ++v)
@@ -191,7 +196,7 @@ __device__ __forceinline__ void store_row(float* M, int64_t row, int64_t pitch, 
 template <int NV>
 __device__ __forceinline__ void atomic_add_row(float* M, int64_t row, int64_t pitch, int d, int lane,
                                                const float (&delta)[NV]) {
-  float* p = M + row * pitch + lane;
+  float* p = M + phys_row(row) * pitch + lane;
 #pragma unroll
   for (int v = 0; v < NV; ++v)
     if (lane + kWave * v < d)
@@ -310,7 +315,7 @@ __device__ __forceinline__ void flush_private(const TrainArgs& a, float* lds, in
     const int p = __builtin_ctzll(m);
     m &= m - 1;
     float* q = lds + p * (NV * kWave) + lane;
-    float* dst = M + (a.priv_lo + p) * a.pitch + lane;
+    float* dst = M + phys_row(a.priv_lo + p) * a.pitch + lane;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       if (lane + kWave * v < a.dim) {
