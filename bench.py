@@ -48,17 +48,22 @@ def parse():
     ap.add_argument("--vocab", type=int, default=1_000_000, help="Zipf rank range (V before min_count)")
     ap.add_argument("--tokens", type=int, default=50_000_000, help="raw tokens per GPU per step")
     ap.add_argument("--sent-len", type=int, default=1000)
+    ap.add_argument("--zipf-s", type=float, default=1.0, help="corpus law p(rank) ~ rank^-s (1 = Zipf)")
     ap.add_argument("--subsample", type=float, default=1e-4)
     ap.add_argument("--min-count", type=int, default=5)
     ap.add_argument("--table-size", type=int, default=100_000_000)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
-    ap.add_argument("--hot-rows", type=int, default=-1,
+    # update policy of the parallel schedule (include/w2v_dev.h); defaults = the library's
+    ap.add_argument("--hot-rows", type=int, default=1000,
                     help="rows updated with atomics (-1 all, 0 none = plain Hogwild RMW, k = k most frequent)")
     ap.add_argument("--private-rows", type=int, default=-1,
                     help="hottest output rows privatised per workgroup in LDS (-1 auto, 0 off)")
-    ap.add_argument("--max-waves", type=int, default=-1,
-                    help="wavefronts in flight (-1: 1024 for hs, all otherwise; 0 = all)")
+    ap.add_argument("--flush-centers", type=int, default=0,
+                    help="workgroup centers between private-row flushes (0 = auto)")
+    ap.add_argument("--private-average", type=float, default=8.0,
+                    help="concurrency the private rows' summed deltas are scaled to (0 = plain sum)")
+    ap.add_argument("--max-waves", type=int, default=0, help="wavefronts in flight (0 = all that fit)")
     ap.add_argument("--own-model", action="store_true",
                     help="N=1 only: let the library allocate the matrices instead of torch")
     ap.add_argument("--sync-every", type=int, default=0,
@@ -107,7 +112,7 @@ def main():
     n_tok = n_sent * args.sent_len
     g = torch.Generator(device=dev)
     g.manual_seed(args.seed * 1000 + rank)
-    p = 1.0 / torch.arange(1, args.vocab + 1, device=dev, dtype=torch.float64)
+    p = torch.arange(1, args.vocab + 1, device=dev, dtype=torch.float64).pow_(-args.zipf_s)
     cdf = torch.cumsum(p, 0)
     cdf /= cdf[-1].clone()
     ranks = torch.empty(n_tok, dtype=torch.int64, device=dev)
@@ -156,7 +161,7 @@ def main():
     tr.set_stream(stream.cuda_stream)
     tr.upload_vocab(keep, bounds, codes, points, coff)
     pitch = (d + 31) // 32 * 32
-    vrows = -(-V // 4096) * 4096 if os.environ.get("W2V_DEV_LIB") else V  # room for the scramble experiment
+    vrows = V
     gW = torch.Generator(device=dev)
     gW.manual_seed(args.seed)  # identical initial replicas on every rank
     W = torch.zeros(vrows, pitch, dtype=torch.float32, device=dev)
@@ -180,7 +185,8 @@ def main():
     tr.set_schedule(N.W2V_SCHED_PARALLEL)
     tr.set_hot_rows(args.hot_rows)
     tr.set_private_rows(args.private_rows)
-    tr.set_max_waves(args.max_waves if args.max_waves >= 0 else (1024 if mode["hs"] else 0))
+    tr.set_private_sync(args.flush_centers, args.private_average)
+    tr.set_max_waves(args.max_waves)
     tr.set_progress(0)
     torch.cuda.synchronize()
     log(f"[bench] resident in HBM ({time.time() - t0:.1f}s)")
@@ -276,6 +282,8 @@ def main():
                                 f"average x{rounds} per step" if world > 1 else "dp1"),
                 "hot_rows": args.hot_rows,
                 "private_rows": args.private_rows,
+                "flush_centers": args.flush_centers,
+                "private_average": args.private_average,
                 "max_waves": args.max_waves,
                 "kept_centers_per_step": int(delta["centers"] / args.steps),
                 "targets_per_step": int(delta["targets"] / args.steps),

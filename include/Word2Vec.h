@@ -97,9 +97,12 @@ class Word2Vec {
                              // stream in the reference's draw order, on one
                              // wavefront (deterministic, equals the reference run
                              // single-threaded up to fp32 summation order)
-  int64_t hot_rows = -1;     // rows updated with device atomics (w2v_dev_set_hot_rows): -1 all
-  int private_rows = -1;     // hottest output rows privatised in LDS (w2v_dev_set_private_rows)
-  int64_t max_waves = -1;    // wavefronts in flight (w2v_dev_set_max_waves); -1 = 1024 for hs, else all
+  // parallel-schedule update policy (include/w2v_dev.h, w2v_dev_set_hot_rows ff.)
+  int64_t hot_rows = 1000;      // rows updated with device atomics: -1 all, 0 none
+  int private_rows = -1;        // hottest output rows privatised in LDS: -1 as many as fit, 0 off
+  int flush_centers = 0;        // workgroup centers between private-row flushes (0 = auto)
+  float private_average = 8.f;  // concurrency the private rows' summed deltas are scaled to (0 = sum)
+  int64_t max_waves = 0;        // wavefronts in flight (0 = as many as fit)
   bool verbose = true;       // progress line per epoch (the reference prints one
                              // every 100 sentences, Word2Vec.cpp:382-386)
   // Train on a corpus that is already token ids (no strings): ids index

@@ -145,27 +145,36 @@ int w2v_dev_synchronize(w2v_dev* h);
 int w2v_dev_read_stats(w2v_dev* h, w2v_dev_stats* stats); /* cumulative; synchronizes */
 int w2v_dev_reset_stats(w2v_dev* h);
 
-/* How row updates land (`row += g*x`, W[center] += grad, C[ctx] += grad):
- * rows of W and C with index < hot_rows (the most frequent words: vocab is
- * sorted by count) and the hot_rows internal Huffman nodes nearest the root
- * use memory-side float atomic adds — no update is lost however many
- * wavefronts hit the row; the other rows use a plain read-modify-write
- * (lock-free Hogwild, an update racing another on the same row can be lost,
- * as between the reference's OpenMP threads). -1 = every row atomic (the
- * default), 0 = none. Same fp32 rounding either way. */
+/* Update policy of the parallel schedule (Hogwild across wavefronts; the
+ * reference's OpenMP threads, Word2Vec.cpp:375-394, race the same way at a far
+ * smaller scale). Three row classes, by frequency rank (the vocab is sorted by
+ * count, Word2Vec.cpp:152):
+ *  - private rows: the n hottest rows of the output layer (the NS target
+ *    matrix — C for skip-gram, W for CBOW — or the n internal Huffman nodes
+ *    nearest the root for HS). Each workgroup (up to 16 wavefronts) keeps its
+ *    pending deltas for them in LDS (ds_add_f32); reads see the HBM value plus
+ *    that delta. Every `flush_centers` centers of the workgroup the deltas go
+ *    to HBM with float atomics, scaled so that a row which k workgroups update
+ *    in one interval moves by at most average_over/k of their sum (local SGD
+ *    on the rows every wavefront touches; without it ~10^4 concurrent stale
+ *    updates of those rows diverge). -1 = as many as fit, at most 64 (default);
+ *    0 = off;
+ *  - hot rows: rows of W and C with index < hot_rows, and the hot_rows internal
+ *    Huffman nodes nearest the root, take memory-side float atomic adds: no
+ *    update is lost however many wavefronts hit the row. -1 = every row,
+ *    0 = none; default 1000;
+ *  - the rest: plain read-modify-write (an update racing another on the same
+ *    row can be lost, as between the reference's threads).
+ * Same fp32 rounding per update in every class. None of this applies to the
+ * sequential schedule (W2V_SCHED_SEQUENTIAL), which is reference-exact. */
 int w2v_dev_set_hot_rows(w2v_dev* h, int64_t hot_rows);
-/* The n hottest rows of the output layer (the NS target matrix, or the
- * internal Huffman nodes nearest the root for HS) are additionally privatised
- * per workgroup: their updates accumulate in LDS (ds_add_f32), reads see the
- * HBM value plus the workgroup's pending delta, and each wavefront flushes the
- * deltas with float atomics after every center (staleness bounded by one
- * center). This takes the same-row atomic serialisation off the few rows
- * every wavefront hits. -1 = as many as fit 40 KiB of LDS per workgroup, at
- * most 32 (default); 0 = off. Not used by the sequential schedule. */
 int w2v_dev_set_private_rows(w2v_dev* h, int32_t n);
-/* Cap on wavefronts in flight in the parallel schedule (0 = as many as fit).
- * Hogwild staleness grows with it: every hierarchical-softmax call updates
- * the Huffman root, so HS needs a cap (~1024) to stay stable. */
+/* flush_centers: workgroup centers between flushes (0 = auto: 256 for NS, 16
+ * for HS); average_over: the concurrency a private row's summed deltas are
+ * scaled down to (default 8; 0 = plain sum). */
+int w2v_dev_set_private_sync(w2v_dev* h, int32_t flush_centers, float average_over);
+/* Cap on wavefronts in flight in the parallel schedule (0 = as many as fit,
+ * the default). Fewer wavefronts, less staleness, less throughput. */
 int w2v_dev_set_max_waves(w2v_dev* h, int64_t n);
 
 /* Word2Vec::train_sentence_* take alpha from the caller (Word2Vec.h:83-84):

@@ -25,7 +25,9 @@ void w2v_model_free(w2v_model* m);
 const char* w2v_model_last_error(w2v_model* m);
 void w2v_model_seed(w2v_model* m, uint32_t seed);               /* generator.seed(seed) */
 void w2v_model_options(w2v_model* m, int32_t gpu_device, int32_t replay_rng, int32_t verbose);
-void w2v_model_update_policy(w2v_model* m, int64_t hot_rows, int32_t private_rows, int64_t max_waves);
+/* Parallel-schedule update policy (Word2Vec.h additive members; include/w2v_dev.h). */
+void w2v_model_update_policy(w2v_model* m, int64_t hot_rows, int32_t private_rows, int32_t flush_centers,
+                             float private_average, int64_t max_waves);
 
 /* Sentences as text: one per line, whitespace-separated tokens (line_docs format). */
 int w2v_model_build_vocab(w2v_model* m, const char* text, int64_t len);

@@ -86,6 +86,7 @@ SIGNATURES = {
     "w2v_dev_set_fixed_alpha": (C.c_int, [_P, _F]),
     "w2v_dev_set_hot_rows": (C.c_int, [_P, _I64]),
     "w2v_dev_set_private_rows": (C.c_int, [_P, _I32]),
+    "w2v_dev_set_private_sync": (C.c_int, [_P, _I32, _F]),
     "w2v_dev_set_max_waves": (C.c_int, [_P, _I64]),
     "w2v_dev_apply_rows": (C.c_int, [_P, _P, _P, _I32, _P, _P, _F, _I32]),
 }
@@ -98,7 +99,7 @@ def load_dev_lib(path: os.PathLike | str | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else Path(os.environ.get("W2V_DEV_LIB", DEV_LIB))
+    p = Path(path) if path else Path(os.environ.get("W2V_DEV_LIB") or DEV_LIB)
     if not p.exists():
         raise RuntimeError(
             f"word2vec_amd: HIP library {p} is missing; build it with "

@@ -65,8 +65,10 @@ struct w2v_dev {
   int64_t pitch = 0;
   int32_t d4 = 0;
   int nv = 1;                 // floats per lane per row (instantiated width >= ceil(d / 64))
-  int64_t hot_rows = -1;      // rows updated with atomics: -1 = all, 0 = none
+  int64_t hot_rows = 1000;    // rows updated with atomics: -1 = all, 0 = none
   int32_t private_rows = -1;  // hottest output rows privatised in LDS: -1 = auto, 0 = off
+  int32_t flush_centers = 0;  // workgroup centers between flushes of the privatised rows (0 = auto)
+  float private_average = 8.0f;  // concurrency the privatised rows' summed deltas are scaled to (0 = plain sum)
   int64_t max_waves = 0;      // cap on concurrently scheduled wavefronts (0 = as many as fit)
   bool need_C = false, need_S = false;
   float* W = nullptr;
@@ -314,30 +316,20 @@ int w2v_dev_upload_table(w2v_dev* h, const uint32_t* table, int64_t n) {
   return W2V_OK;
 }
 
-// Model allocation flavour (experiments): W2V_MATRIX_ALLOC=uncached|finegrained.
-static hipError_t model_malloc(float** p, size_t bytes) {
-  const char* mode = std::getenv("W2V_MATRIX_ALLOC");
-  if (mode && !std::strcmp(mode, "uncached"))
-    return hipExtMallocWithFlags(reinterpret_cast<void**>(p), bytes, hipDeviceMallocUncached);
-  if (mode && !std::strcmp(mode, "finegrained"))
-    return hipExtMallocWithFlags(reinterpret_cast<void**>(p), bytes, hipDeviceMallocFinegrained);
-  return hipMalloc(p, bytes);
-}
-
 static int ensure_model(w2v_dev* h) {
   if (h->V < 1) return fail(W2V_ERR_STATE, "upload the vocab before the model");
   const size_t rows_bytes = (size_t)h->V * h->pitch * sizeof(float);
   if (!h->W) {
-    HIP_TRY(model_malloc(&h->W, rows_bytes));
+    HIP_TRY(hipMalloc(&h->W, rows_bytes));
     HIP_TRY(hipMemset(h->W, 0, rows_bytes));
   }
   if (h->need_C && !h->C) {
-    HIP_TRY(model_malloc(&h->C, rows_bytes));
+    HIP_TRY(hipMalloc(&h->C, rows_bytes));
     HIP_TRY(hipMemset(h->C, 0, rows_bytes));
   }
   if (h->need_S && !h->S) {
     const size_t sb = (size_t)(h->V > 1 ? h->V - 1 : 1) * h->pitch * sizeof(float);
-    HIP_TRY(model_malloc(&h->S, sb));
+    HIP_TRY(hipMalloc(&h->S, sb));
     HIP_TRY(hipMemset(h->S, 0, sb));
   }
   return W2V_OK;
@@ -516,20 +508,32 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     a.hot_s = (h->V - 1) - hot;  // the top `hot` internal nodes (the root is V-2)
   }
   a.strict = h->sched == W2V_SCHED_SEQUENTIAL ? 1 : 0;
-  a.fresh_all = std::getenv("W2V_FRESH_LOADS") ? 1 : 0;  // experiment: every row gather bypasses L1
-  a.flush_every = 1;
-  if (const char* f = std::getenv("W2V_FLUSH_EVERY")) a.flush_every = std::atoi(f) > 0 ? std::atoi(f) : 1;
+  // Workgroup shape: up to 16 waves share the LDS-privatised rows (kMaxBlock);
+  // under a wave cap, narrower workgroups so the capped grid still spans the CUs.
+  const int max_wpb = (h->nv <= 6 ? 1024 : 256) / w2v::kWave;
+  int wpb = max_wpb;
+  if (h->max_waves > 0) {
+    int64_t per = h->max_waves / (h->n_cu > 0 ? h->n_cu : 1);
+    wpb = 1;
+    while (wpb * 2 <= max_wpb && wpb * 2 <= per) wpb *= 2;
+  }
+  // Flush interval of the privatised rows, in centers of the workgroup (about
+  // 16 centers per wave for NS, 1 per wave for HS whose top nodes every
+  // update touches), and the averaging of their deltas (flush_private).
+  a.flush_every = h->flush_centers > 0 ? h->flush_centers : (h->cfg.hs ? 16 : 256);
+  a.priv_avg = h->private_average;
   // LDS privatisation of the output layer's hottest rows (the NS target matrix
   // — C for skip-gram, W for CBOW — or the top of the Huffman tree for HS):
-  // as many rows as fit 40 KiB per workgroup (4 workgroups per CU), <= 64.
+  // as many rows as fit 10 KiB per wave of the workgroup, <= 64 (the dirty mask).
   size_t lds_bytes = 0;
   a.priv_M = nullptr;
   a.priv_lo = 0;
   a.priv_n = 0;
   {
     const int64_t row_bytes = (int64_t)h->nv * w2v::kWave * (int64_t)sizeof(float);
-    int64_t fit = (40 * 1024 - 16) / row_bytes;
-    if (fit > 32) fit = 32;
+    const int64_t budget = std::min<int64_t>(160 * 1024, 10 * 1024 * (int64_t)wpb) - 16 - 4 * 64;
+    int64_t fit = budget / row_bytes;
+    if (fit > 64) fit = 64;
     int64_t P = h->private_rows < 0 ? fit : (h->private_rows < fit ? h->private_rows : fit);
     const bool hs = h->cfg.hs != 0;
     const int64_t avail = hs ? h->V - 1 : h->V;
@@ -539,26 +543,27 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
       a.priv_M = hs ? h->S : (h->cfg.cbow ? h->W : h->C);
       a.priv_lo = hs ? avail - P : 0;  // HS: the P internal nodes nearest the root (V-2)
       a.priv_n = (int32_t)P;
-      lds_bytes = (size_t)(P * row_bytes) + 16;  // + the dirty mask
+      lds_bytes = (size_t)(P * row_bytes) + 16 + (size_t)P * 4;  // + mask, counts, per-row hits
     }
   }
   KernelFn fn = kernel_for(h);
   HIP_TRY(hipMemsetAsync(h->work, 0, sizeof(unsigned int), h->stream));
   dim3 grid(1), block(64);
   if (h->sched == W2V_SCHED_PARALLEL) {
+    const int threads = wpb * w2v::kWave;
     int per_cu = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds_bytes));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds_bytes));
     if (per_cu < 1) per_cu = 1;
     const int64_t resident = (int64_t)per_cu * h->n_cu;
-    const int64_t need = (count + 3) / 4;
+    const int64_t need = (count + wpb - 1) / wpb;
     int64_t g = need < resident ? need : resident;
-    if (h->max_waves > 0 && (h->max_waves + 3) / 4 < g) g = (h->max_waves + 3) / 4;
+    if (h->max_waves > 0 && (h->max_waves + wpb - 1) / wpb < g) g = (h->max_waves + wpb - 1) / wpb;
     if (const char* cap = std::getenv("W2V_DEBUG_MAX_BLOCKS")) {  // diagnostics only
       const int64_t c = std::atoll(cap);
       if (c > 0 && c < g) g = c;
     }
     grid = dim3((unsigned)g);
-    block = dim3(256);
+    block = dim3(threads);
   }
   hipLaunchKernelGGL(fn, grid, block, lds_bytes, h->stream, a);
   HIP_TRY(hipGetLastError());
@@ -638,6 +643,15 @@ int w2v_dev_set_private_rows(w2v_dev* h, int32_t n) {
   if (!h) return fail(W2V_ERR_ARG, "null handle");
   if (n < -1) return fail(W2V_ERR_ARG, "private_rows must be >= -1");
   h->private_rows = n;
+  return W2V_OK;
+}
+
+int w2v_dev_set_private_sync(w2v_dev* h, int32_t flush_centers, float average_over) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (flush_centers < 0) return fail(W2V_ERR_ARG, "flush_centers must be >= 0");
+  if (!(average_over >= 0.0f)) return fail(W2V_ERR_ARG, "average_over must be >= 0");
+  h->flush_centers = flush_centers;
+  h->private_average = average_over;
   return W2V_OK;
 }
 

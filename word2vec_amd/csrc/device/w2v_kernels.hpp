@@ -46,6 +46,11 @@
 namespace w2v {
 
 constexpr int kWave = 64;
+// Largest workgroup per row width: up to 16 waves share one LDS region of
+// privatised rows while the register budget (<=128 VGPRs at 4 waves/SIMD)
+// holds; wider rows keep 4-wave workgroups.
+template <int NV>
+constexpr int kMaxBlock = NV <= 6 ? 1024 : 256;
 
 struct TrainArgs {
   float* W;
@@ -84,8 +89,8 @@ struct TrainArgs {
   const float* priv_M;         // output matrix whose hottest rows are privatised in LDS (or null)
   int64_t priv_lo;             // privatised rows [priv_lo, priv_lo + priv_n)
   int32_t priv_n;
-  int32_t fresh_all;           // every row gather uses L1-bypassing loads
-  int32_t flush_every;         // a wavefront flushes the privatised deltas every this many centers
+  float priv_avg;              // > 0: average, not sum, the workgroups' deltas of a privatised row (see flush_private)
+  int32_t flush_every;         // the privatised deltas are flushed every this many centers of the workgroup
 };
 
 struct Counters {
@@ -156,15 +161,10 @@ __device__ __forceinline__ uint32_t philox_table_pos(const TrainArgs& a, uint32_
 // ---------------------------------------------------------------------------
 // Row I/O: a row is NV floats per lane, element lane + 64 v (v < NV).
 // ---------------------------------------------------------------------------
-#ifdef W2V_SCRAMBLE  // experiment build: spread consecutive rows 1031 slots apart inside 4096-row blocks
-__device__ __forceinline__ int64_t phys_row(int64_t r) { return (r & ~4095LL) | (((r & 4095) * 1031) & 4095); }
-#else
-__device__ __forceinline__ int64_t phys_row(int64_t r) { return r; }
-#endif
 template <int NV>
 __device__ __forceinline__ void load_row(const float* M, int64_t row, int64_t pitch, int d, int lane,
                                          bool fresh, float (&r)[NV]) {
-  const float* p = M + phys_row(row) * pitch + lane;
+  const float* p = M + row * pitch + lane;
   if (fresh) {  // agent-scope relaxed loads: global_load_dword sc1, bypass the CU's L1
 #pragma unroll
     for (int v = 0; v < NV; ++v)
@@ -179,24 +179,18 @@ __device__ __forceinline__ void load_row(const float* M, int64_t row, int64_t pi
 
 template <int NV>
 __device__ __forceinline__ void store_row(float* M, int64_t row, int64_t pitch, int d, int lane,
-                                          const float (&r)[NV], bool wt = false) {
-  float* p = M + phys_row(row) * pitch + lane;
-  if (wt) {  // global_store_dword sc1: write through and drop the line from this XCD's L2
+                                          const float (&r)[NV]) {
+  float* p = M + row * pitch + lane;
 #pragma unroll
-    for (int v = 0; v < NV; ++v)
-      if (lane + kWave * v < d) __hip_atomic_store(p + kWave * v, r[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-#pragma unroll
-    for (int v = 0; v < NV; ++v)
-      if (lane + kWave * v < d) p[kWave * v] = r[v];
-  }
+  for (int v = 0; v < NV; ++v)
+    if (lane + kWave * v < d) p[kWave * v] = r[v];
 }
 
 // row += delta, memory-side (no-return global_atomic_add_f32, 256 contiguous B per instruction)
 template <int NV>
 __device__ __forceinline__ void atomic_add_row(float* M, int64_t row, int64_t pitch, int d, int lane,
                                                const float (&delta)[NV]) {
-  float* p = M + phys_row(row) * pitch + lane;
+  float* p = M + row * pitch + lane;
 #pragma unroll
   for (int v = 0; v < NV; ++v)
     if (lane + kWave * v < d)
@@ -206,15 +200,15 @@ __device__ __forceinline__ void atomic_add_row(float* M, int64_t row, int64_t pi
 // M[row] += delta: atomically for hot rows; else read-modify-write (Hogwild).
 template <int NV>
 __device__ __forceinline__ void add_to_row(float* M, int64_t row, bool hot, int64_t pitch, int d, int lane,
-                                           const float (&delta)[NV], bool fresh = false) {
+                                           const float (&delta)[NV]) {
   if (hot) {
     atomic_add_row<NV>(M, row, pitch, d, lane, delta);
   } else {
     float cur[NV];
-    load_row<NV>(M, row, pitch, d, lane, fresh, cur);
+    load_row<NV>(M, row, pitch, d, lane, false, cur);
 #pragma unroll
     for (int v = 0; v < NV; ++v) cur[v] += delta[v];
-    store_row<NV>(M, row, pitch, d, lane, cur, fresh);
+    store_row<NV>(M, row, pitch, d, lane, cur);
   }
 }
 
@@ -229,7 +223,7 @@ template <int NV, int MAXT, bool HSF>
 __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, int lane, int T, int row_l,
                                               int code_l, int t0, const float (&x)[NV], float (&g)[NV],
                                               float alpha, int64_t hot_lo, int64_t hot_hi, float* lds,
-                                              int64_t priv_lo, int64_t priv_n, bool fresh = false) {
+                                              int64_t priv_lo, int64_t priv_n) {
   float r[MAXT][NV];
   int rows[MAXT];
   bool hot[MAXT], priv[MAXT];
@@ -238,7 +232,7 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
     rows[t] = readlane_i(row_l, t0 + t);
     priv[t] = lds != nullptr && rows[t] >= priv_lo && rows[t] < priv_lo + priv_n;
     hot[t] = !priv[t] && rows[t] >= hot_lo && rows[t] < hot_hi;
-    if (t < T) load_row<NV>(M, rows[t], pitch, d, lane, hot[t] || priv[t] || fresh, r[t]);
+    if (t < T) load_row<NV>(M, rows[t], pitch, d, lane, hot[t] || priv[t], r[t]);
   }
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) {  // privatised rows: global value + this workgroup's pending delta
@@ -291,7 +285,7 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
       } else {
 #pragma unroll
         for (int v = 0; v < NV; ++v) r[t][v] += delta[v];
-        store_row<NV>(M, rows[t], pitch, d, lane, r[t], fresh);
+        store_row<NV>(M, rows[t], pitch, d, lane, r[t]);
       }
     }
   }
@@ -306,22 +300,42 @@ template <int NV>
 __device__ __forceinline__ void flush_private(const TrainArgs& a, float* lds, int lane) {
   if (lds == nullptr) return;
   unsigned long long* dirty = reinterpret_cast<unsigned long long*>(lds + a.priv_n * (NV * kWave));
+  unsigned* tail = reinterpret_cast<unsigned*>(dirty);  // [0,1] dirty mask, [2] centers, [3] flushes, [4+p] hits
   unsigned long long m = 0;
   if (lane == 0) m = atomicExch(dirty, 0ull);
   m = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(m >> 32)) << 32) |
       (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)m);
+  if (m == 0) return;
+  // Averaging (priv_avg = S > 0): a row that n workgroups update within one
+  // flush interval receives the mean of their deltas scaled to at most S
+  // concurrent contributions (local SGD on the few rows every wave updates),
+  // with n = workgroups x this workgroup's fraction of flushes touching it.
+  float flushes = 1.0f;
+  if (a.priv_avg > 0.0f) {
+    unsigned fl = 0;
+    if (lane == 0) fl = atomicAdd(tail + 3, 1u) + 1u;
+    flushes = (float)(unsigned)__builtin_amdgcn_readfirstlane((int)fl);
+  }
   float* M = const_cast<float*>(a.priv_M);
   while (m) {
     const int p = __builtin_ctzll(m);
     m &= m - 1;
+    float sc = 1.0f;
+    if (a.priv_avg > 0.0f) {
+      unsigned h = 0;
+      if (lane == 0) h = atomicAdd(tail + 4 + p, 1u) + 1u;
+      const float hits = (float)(unsigned)__builtin_amdgcn_readfirstlane((int)h);
+      const float n = (float)gridDim.x * hits / flushes;
+      sc = 1.0f / fmaxf(1.0f, n / a.priv_avg);
+    }
     float* q = lds + p * (NV * kWave) + lane;
-    float* dst = M + phys_row(a.priv_lo + p) * a.pitch + lane;
+    float* dst = M + (a.priv_lo + p) * a.pitch + lane;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       if (lane + kWave * v < a.dim) {
         const float val = atomicExch(q + kWave * v, 0.0f);
         if (val != 0.0f)
-          (void)__hip_atomic_fetch_add(dst + kWave * v, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          (void)__hip_atomic_fetch_add(dst + kWave * v, val * sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
@@ -341,7 +355,7 @@ __device__ __forceinline__ void hs_word(const TrainArgs& a, int word, int lane, 
     for (int t0 = 0; t0 < rem; t0 += MAXT) {
       if (a.strict) drain_vmem();
       apply_targets<NV, MAXT, true>(a.S, a.pitch, a.dim, lane, min(MAXT, rem - t0), pt_l, cd_l, t0, x, g,
-                                    alpha, a.hot_s, INT64_MAX, plds, a.priv_lo, a.priv_n, a.fresh_all != 0);
+                                    alpha, a.hot_s, INT64_MAX, plds, a.priv_lo, a.priv_n);
     }
     cnt.targets += (unsigned long long)rem;
   }
@@ -377,7 +391,7 @@ __device__ __forceinline__ void ns_word(const TrainArgs& a, float* M, int word, 
   for (int t0 = 0; t0 < T; t0 += MAXT) {
     if (a.strict) drain_vmem();
     apply_targets<NV, MAXT, false>(M, a.pitch, a.dim, lane, min(MAXT, T - t0), tgt_l, code_l, t0, x, g, alpha,
-                                   0, a.hot_wc, plds, a.priv_lo, a.priv_n, a.fresh_all != 0);
+                                   0, a.hot_wc, plds, a.priv_lo, a.priv_n);
   }
   cnt.targets += (unsigned long long)T;
 }
@@ -413,7 +427,7 @@ __device__ __forceinline__ void sg_center(const TrainArgs& a, float* lds, const 
   const bool hot_c = c < a.hot_wc;
   float x[NV], g[NV];
   if (a.strict) drain_vmem();
-  load_row<NV>(a.W, c, a.pitch, a.dim, lane, hot_c || a.fresh_all, x);
+  load_row<NV>(a.W, c, a.pitch, a.dim, lane, hot_c, x);
 #pragma unroll
   for (int v = 0; v < NV; ++v) g[v] = 0.f;
   const int ctx_l = (lane < span) ? sent[lo + lane] : 0;
@@ -439,7 +453,7 @@ __device__ __forceinline__ void sg_center(const TrainArgs& a, float* lds, const 
     }
     ++slot;
   }
-  add_to_row<NV>(a.W, c, hot_c, a.pitch, a.dim, lane, g, a.fresh_all != 0);  // W.row(center) += neu1_grad (:351)
+  add_to_row<NV>(a.W, c, hot_c, a.pitch, a.dim, lane, g);  // W.row(center) += neu1_grad (:351)
 }
 
 // ---------------------------------------------------------------------------
@@ -494,7 +508,7 @@ __device__ __forceinline__ void cbow_center(const TrainArgs& a, float* lds, cons
     for (int t = 0; t < MAXT; ++t)
       if (r0 + t < U) {
         const int row = readlane_i(sid, r0 + t);
-        load_row<NV>(a.C, row, a.pitch, a.dim, lane, row < a.hot_wc || a.fresh_all, rr[t]);
+        load_row<NV>(a.C, row, a.pitch, a.dim, lane, row < a.hot_wc, rr[t]);
       }
 #pragma unroll
     for (int t = 0; t < MAXT; ++t)
@@ -521,21 +535,28 @@ __device__ __forceinline__ void cbow_center(const TrainArgs& a, float* lds, cons
   }
   for (int r = 0; r < U; ++r) {  // C.row(id) += neu1_grad for every unique id (:315)
     const int row = readlane_i(sid, r);
-    add_to_row<NV>(a.C, row, row < a.hot_wc, a.pitch, a.dim, lane, g, a.fresh_all != 0);
+    add_to_row<NV>(a.C, row, row < a.hot_wc, a.pitch, a.dim, lane, g);
   }
 }
 
 template <int NV, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY>
 __device__ __forceinline__ void center(const TrainArgs& a, float* lds, const int32_t* sent, int len, int i, int c,
                                        int rw, uint32_t s, float alpha, const uint32_t*& rp, Counters& cnt,
-                                       int lane, int& since_flush) {
+                                       int lane) {
   if (CBOW)
     cbow_center<NV, MAXT, HS, NS, REPLAY>(a, lds, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
   else
     sg_center<NV, MAXT, HS, NS, REPLAY>(a, lds, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
-  if (++since_flush >= a.flush_every) {  // bounded staleness: deltas live for flush_every centers
-    flush_private<NV>(a, lds, lane);
-    since_flush = 0;
+  if (lds != nullptr) {
+    // Bounded staleness with aggregation: the workgroup's waves share one
+    // center count, and the wave that completes every flush_every-th center
+    // drains the deltas all of them accumulated (one atomic per dirty row
+    // instead of one per update and wave).
+    unsigned* done = reinterpret_cast<unsigned*>(lds + a.priv_n * (NV * kWave) + 2);
+    unsigned n = 0;
+    if (lane == 0) n = atomicAdd(done, 1u) + 1u;
+    n = (unsigned)__builtin_amdgcn_readfirstlane((int)n);
+    if (n % (unsigned)a.flush_every == 0u) flush_private<NV>(a, lds, lane);
   }
 }
 
@@ -543,16 +564,15 @@ __device__ __forceinline__ void center(const TrainArgs& a, float* lds, const int
 // The epoch kernel: wavefronts dequeue sentences (Word2Vec.cpp:375-394).
 // ---------------------------------------------------------------------------
 template <int NV, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY>
-__global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
+__global__ __launch_bounds__(kMaxBlock<NV>) void train_epoch_kernel(TrainArgs a) {
   extern __shared__ float w2v_lds[];
   const int lane = lane_id();
   float* lds = a.priv_n > 0 ? w2v_lds : nullptr;
   if (lds) {
-    for (int k = threadIdx.x; k < a.priv_n * NV * kWave + 2; k += blockDim.x) lds[k] = 0.0f;  // deltas + dirty mask
+    for (int k = threadIdx.x; k < a.priv_n * (NV * kWave + 1) + 4; k += blockDim.x) lds[k] = 0.0f;  // deltas + tail
     __syncthreads();
   }
   Counters cnt;
-  int since_flush = 0;
   float alpha = a.init_alpha;
   bool first = true;
   const uint32_t wmax = (uint32_t)(a.window < 1 ? 1 : a.window);
@@ -584,8 +604,7 @@ __global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
         if (a.keep[c] < u) continue;
         const int rw = (int)rp[0];
         ++rp;
-        center<NV, MAXT, CBOW, HS, NS, REPLAY>(a, lds, sent, len, i, c, rw, (uint32_t)s, alpha, rp, cnt, lane,
-                                                since_flush);
+        center<NV, MAXT, CBOW, HS, NS, REPLAY>(a, lds, sent, len, i, c, rw, (uint32_t)s, alpha, rp, cnt, lane);
       }
     } else {
       for (int i0 = 0; i0 < len; i0 += kWave) {
@@ -603,7 +622,7 @@ __global__ __launch_bounds__(256) void train_epoch_kernel(TrainArgs a) {
           kept &= kept - 1;
           const int c = readlane_i(c_l, b), rw = readlane_i(rw_l, b);
           center<NV, MAXT, CBOW, HS, NS, REPLAY>(a, lds, sent, len, i0 + b, c, rw, (uint32_t)s, alpha, rp, cnt,
-                                                  lane, since_flush);
+                                                  lane);
         }
       }
     }

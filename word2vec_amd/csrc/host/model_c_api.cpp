@@ -71,9 +71,12 @@ void w2v_model_options(w2v_model* m, int32_t gpu, int32_t replay, int32_t verbos
   m->w.verbose = verbose != 0;
 }
 
-void w2v_model_update_policy(w2v_model* m, int64_t hot_rows, int32_t private_rows, int64_t max_waves) {
+void w2v_model_update_policy(w2v_model* m, int64_t hot_rows, int32_t private_rows, int32_t flush_centers,
+                             float private_average, int64_t max_waves) {
   m->w.hot_rows = hot_rows;
   m->w.private_rows = private_rows;
+  m->w.flush_centers = flush_centers;
+  m->w.private_average = private_average;
   m->w.max_waves = max_waves;
 }
 

@@ -173,12 +173,18 @@ class DeviceTrainer:
         self._chk(self.lib.w2v_dev_reset_stats(self.h), "w2v_dev_reset_stats")
 
     def set_hot_rows(self, hot_rows: int):
-        """Rows updated with atomics: -1 = all (default), 0 = none (plain Hogwild RMW), k = the k most frequent."""
+        """Rows updated with atomics: -1 = all, 0 = none (plain Hogwild RMW), k = the k most frequent (default 1000)."""
         self._chk(self.lib.w2v_dev_set_hot_rows(self.h, int(hot_rows)), "w2v_dev_set_hot_rows")
 
     def set_private_rows(self, n: int):
         """Hottest output rows privatised per workgroup in LDS: -1 auto (default), 0 off."""
         self._chk(self.lib.w2v_dev_set_private_rows(self.h, int(n)), "w2v_dev_set_private_rows")
+
+    def set_private_sync(self, flush_centers: int = 0, average_over: float = 8.0):
+        """Workgroup centers between flushes of the private rows (0 = auto) and the
+        concurrency their summed deltas are scaled to (0 = plain sum); include/w2v_dev.h."""
+        self._chk(self.lib.w2v_dev_set_private_sync(self.h, int(flush_centers), float(average_over)),
+                  "w2v_dev_set_private_sync")
 
     def set_max_waves(self, n: int):
         """Cap on wavefronts in flight (0 = as many as fit)."""
