@@ -33,7 +33,10 @@ MODES = {
     "sg_hs": dict(cbow=False, hs=True),
     "cbow_ns": dict(cbow=True, hs=False),
     "cbow_hs": dict(cbow=True, hs=True),
+    # configs[4]: shared-negatives minibatch SGNS on the matrix cores (run with --dim 512 --negative 15)
+    "sg_sn": dict(cbow=False, hs=False, shared=True),
 }
+MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X dense f32-input MFMA (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -160,7 +163,7 @@ def main():
     torch.cuda.set_stream(stream)
     tr.set_stream(stream.cuda_stream)
     tr.upload_vocab(keep, bounds, codes, points, coff)
-    pitch = (d + 31) // 32 * 32
+    pitch = (d + 63) // 64 * 64
     vrows = V
     gW = torch.Generator(device=dev)
     gW.manual_seed(args.seed)  # identical initial replicas on every rank
@@ -182,6 +185,8 @@ def main():
                       S.data_ptr() if S is not None else None, pitch)
     tr.upload_corpus(ids_h, soff_h, n_tok * world)  # alpha follows the global raw-token total
     tr.set_rng(N.W2V_RNG_PHILOX, (args.seed << 32) | (rank + 1))
+    if mode.get("shared"):
+        tr.set_update(N.W2V_UPDATE_SHARED_NEGATIVES)
     tr.set_schedule(N.W2V_SCHED_PARALLEL)
     tr.set_hot_rows(args.hot_rows)
     tr.set_private_rows(args.private_rows)
@@ -239,7 +244,7 @@ def main():
 
     value = words_total / elapsed
     # algorithmic HBM bytes per launch: fp32 rows read+written
-    if mode["cbow"]:
+    if mode["cbow"] or mode.get("shared"):  # unique context rows (CBOW inputs / minibatch W rows)
         row_moves = 2 * delta["contexts"] + 2 * delta["targets"]
     else:
         row_moves = 2 * delta["centers"] + 2 * delta["targets"]
@@ -251,6 +256,13 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, bytes_per_launch),
                 "kernel": "train_epoch_kernel", "avg_launch_ms": round(avg_kernel_s * 1e3, 3),
                 "algorithmic_bytes_per_launch": int(bytes_per_launch)}
+    if mode.get("shared"):
+        # MFMA work issued per kept center: three 16 x 16 x pitch f32 GEMMs (L, dW, dC)
+        flops = 3 * 2 * 16 * 16 * pitch * delta["centers"] / n_launch
+        tf = flops / avg_kernel_s / 1e12
+        roofline["kernel"] = "train_shared_neg_kernel"
+        roofline["mfma"] = {"issued_tflops": round(tf, 2), "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                            "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 4), "dtype": "f32 (v_mfma_f32_16x16x4_f32)"}
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -258,7 +270,8 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": "trained words/sec, dim=300 SGNS (per-GPU replica, RCCL model averaging for N>1)",
+            "metric": (f"trained words/sec, dim={d} SGNS" + (" shared-negatives minibatch" if mode.get("shared") else "")
+                       + " (per-GPU replica, RCCL model averaging for N>1)"),
             "value": round(value, 1),
             "unit": "words/s",
             "n_gpus": world,
@@ -272,8 +285,9 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": f"{args.mode} neg{neg} d{d} w{args.window} subsample {args.subsample} min_count "
-                            f"{args.min_count}; synthetic Zipf(s=1) over {args.vocab} ranks standing in for 1B-Word "
-                            f"(configs[2]); {args.sent_len}-token sentences",
+                            f"{args.min_count}; synthetic Zipf(s={args.zipf_s:g}) over {args.vocab} ranks "
+                            + ("(configs[4], shared-negatives minibatch)" if mode.get("shared") else
+                               "standing in for 1B-Word (configs[2])") + f"; {args.sent_len}-token sentences",
                 "tokens_per_gpu_per_step": n_tok,
                 "in_vocab_tokens_per_gpu_per_step": int(ids_h.size),
                 "vocab_size": V,
@@ -336,7 +350,9 @@ def cpu_baseline(args, counts_v, ids_h, soff_h, neg, mode):
     dt = time.perf_counter() - t
     return {"value": round(w / dt, 1), "unit": "words/s", "cores": threads, "kind": "port",
             "sample": f"{n} sentences ({w} in-vocab tokens) of the same shard, {dt:.1f}s, oracle OpenMP loop "
-                      f"(per-call hash map / set, static schedule, per-thread mt19937)"}
+                      f"(per-call hash map / set, static schedule, per-thread mt19937)"
+                      + ("; the reference's per-pair update: the shared-negatives minibatch has no reference CPU path"
+                         if mode.get("shared") else "")}
 
 
 if __name__ == "__main__":

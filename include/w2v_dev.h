@@ -15,8 +15,9 @@
  * handle's HIP stream (w2v_dev_set_stream).
  *
  * Device layout (HBM): W, C and synapses1 are row-major fp32 with a row pitch
- * of round_up(word_dim, 32) floats (128-B aligned rows; a kernel lane owns
- * elements lane + 64 v of a row); the unigram table is
+ * of round_up(word_dim, 64) floats (256-B aligned rows; a per-pair kernel lane
+ * owns elements lane + 64 v of a row, the shared-negatives kernel's wave w the
+ * columns [pitch/4 w, pitch/4 (w+1))); the unigram table is
  * uint32[table_size]; sample probabilities fp32[V]; Huffman paths are CSR
  * (uint8 codes, int32 points, int64 offsets); the corpus is int32 token ids
  * with int64 sentence offsets.
@@ -43,6 +44,11 @@ extern "C" {
 /* Schedules. */
 #define W2V_SCHED_PARALLEL 0   /* one wavefront per sentence, Hogwild across sentences */
 #define W2V_SCHED_SEQUENTIAL 1 /* one wavefront walks the sentences in order: deterministic */
+
+/* Update formulations (w2v_dev_set_update). */
+#define W2V_UPDATE_PER_PAIR 0         /* the reference's: each (center, context) pair its own NS/HS call */
+#define W2V_UPDATE_SHARED_NEGATIVES 1 /* minibatch SGNS: one window's contexts x (center + shared
+                                         negatives) as dense MFMA GEMMs (BASELINE configs[4]) */
 
 typedef struct w2v_dev w2v_dev; /* opaque handle */
 
@@ -176,6 +182,19 @@ int w2v_dev_set_private_sync(w2v_dev* h, int32_t flush_centers, float average_ov
 /* Cap on wavefronts in flight in the parallel schedule (0 = as many as fit,
  * the default). Fewer wavefronts, less staleness, less throughput. */
 int w2v_dev_set_max_waves(w2v_dev* h, int64_t n);
+
+/* Update formulation of the training kernels. W2V_UPDATE_PER_PAIR (default)
+ * is the reference's train_sentence_sg/cbow (Word2Vec.cpp:273-353).
+ * W2V_UPDATE_SHARED_NEGATIVES is the minibatch skip-gram of BASELINE
+ * configs[4], a new formulation with no reference counterpart (restated in
+ * oracle/w2v_oracle.cpp:sgsn_sentence): per kept center, the unique context
+ * ids of its (shrunk) window are the inputs (W rows, weighted by multiplicity),
+ * the center plus `negative` draws shared by the whole window the outputs (C
+ * rows), and the window's updates are the three GEMMs L = W_in C_out^T,
+ * dW_in = E C_out, dC_out = E^T W_in on the matrix cores. Skip-gram NS only,
+ * negative <= 15, window <= 8, Philox draws, row pitch 64 * {1..8,10,12,16}
+ * floats (W2V_ERR_UNSUPPORTED otherwise). */
+int w2v_dev_set_update(w2v_dev* h, int32_t mode);
 
 /* Word2Vec::train_sentence_* take alpha from the caller (Word2Vec.h:83-84):
  * alpha > 0 makes every following epoch use it instead of the schedule of

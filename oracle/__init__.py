@@ -55,6 +55,7 @@ _SIG = {
     "orc_train_replay": (None, [_P, _I32, _P, _P, _P, _I64]),
     "orc_train_philox": (None, [_P, _I32, _I32, _P, _U64, _I64]),
     "orc_philox": (None, [_P, _U64, _P]),
+    "orc_set_shared_negatives": (None, [_P, _I32]),
     "orc_train_omp": (_I64, [_P, _I32, _I64, _U32]),
     "orc_set_vocab_counts": (None, [_P, _P, _I64]),
     "orc_set_samples": (None, [_P, _P, _P, _I64, _I64]),
@@ -202,6 +203,10 @@ class Oracle:
     def train_philox(self, epoch0, epochs, orders, key, cw0=0):
         orders = np.ascontiguousarray(orders, np.int64)
         self.L.orc_train_philox(self.h, epoch0, epochs, _p(orders), key, cw0)
+
+    def set_shared_negatives(self, on: bool = True):
+        """Shared-negatives minibatch skip-gram (configs[4]) for later training calls."""
+        self.L.orc_set_shared_negatives(self.h, int(bool(on)))
 
     def train_omp(self, threads: int, n_sent_limit: int, seed: int = 1) -> int:
         return self.L.orc_train_omp(self.h, threads, n_sent_limit, seed)

@@ -78,6 +78,7 @@ struct Orc {
   std::vector<int64_t> orders;      // [epoch * n_sent + i]
   int64_t train_words = 0, current_words = 0;
   float last_alpha = 0.f;
+  bool shared_negatives = false;  // sgsn_sentence instead of sg_sentence (configs[4])
 };
 
 // ---------------------------------------------------------------------------
@@ -442,6 +443,78 @@ void cbow_sentence(Orc& m, const int32_t* sent, int len, float alpha, D& dr, int
   }
 }
 
+// Shared-negatives minibatch skip-gram (BASELINE configs[4]; the formulation
+// of Ji et al., "Parallelizing Word2Vec in Shared and Distributed Memory",
+// 2016). NOT a reference function: the reference has no minibatch path. It
+// keeps the reference's subsampling, window shrink, alpha schedule and NS
+// arithmetic (Word2Vec.cpp:251-271, 319-353) but batches one window into a
+// dense update:
+//   inputs  u: the unique context ids of the window (W rows), multiplicity m_u
+//   outputs t: the center word (label 1, C row) and `negative` draws shared by
+//              the whole window (label 0; a draw equal to the center or to an
+//              earlier draw is dropped — the set semantics of :253-257)
+//   L[u][t] = W[u].C[t];  E[u][t] = m_u * (label_t - sigma(L)) * alpha
+//   W[u] += sum_t E[u][t] C[t];  C[t] += sum_u E[u][t] W[u]   (pre-update rows)
+// i.e. the simultaneous update of every (context, output) pair of the window,
+// with the input/output roles of word2vec.c (context predicts center); the
+// reference's own per-pair loop has them the other way round (:339-347),
+// which gives the same pair set over a symmetric window.
+template <class D>
+void sgsn_sentence(Orc& m, const int32_t* sent, int len, float alpha, D& dr, int64_t sid) {
+  const int d = m.cfg.dim, win = m.cfg.window, K = m.cfg.negative;
+  std::vector<int> in_id, in_m, out_id, out_lab;
+  std::vector<float> E, dW, dC;
+  for (int i = 0; i < len; ++i) {
+    const int c = sent[i];
+    dr.at(sid, i);
+    if (m.keep[c] < dr.uniform()) continue;
+    const int rw = dr.window_shrink();
+    const int lo = std::max(0, i - win + rw), hi = std::min(len, i + win + 1 - rw);
+    in_id.clear(); in_m.clear();
+    for (int j = lo; j < hi; ++j) {
+      if (j == i) continue;
+      size_t u = 0;
+      while (u < in_id.size() && in_id[u] != sent[j]) ++u;
+      if (u == in_id.size()) { in_id.push_back(sent[j]); in_m.push_back(0); }
+      in_m[u] += 1;
+    }
+    if (in_id.empty()) continue;
+    out_id.assign(1, c);
+    out_lab.assign(1, 1);
+    for (int k = 0; k < K; ++k) {
+      const int n = (int)m.table[dr.table_pos(0, k)];
+      bool seen = false;
+      for (int o : out_id) seen = seen || (o == n);
+      if (!seen) { out_id.push_back(n); out_lab.push_back(0); }
+    }
+    const size_t M = in_id.size(), T = out_id.size();
+    E.assign(M * T, 0.0f);
+    for (size_t u = 0; u < M; ++u)
+      for (size_t t = 0; t < T; ++t) {
+        float f = row_dot(&m.W[(size_t)in_id[u] * d], &m.C[(size_t)out_id[t] * d], d);
+        f = 1.0 / (1 + std::exp(-f));
+        const float g = (out_lab[t] - f) * alpha;
+        E[u * T + t] = (float)in_m[u] * g;
+      }
+    dW.assign(M * d, 0.0f);
+    dC.assign(T * d, 0.0f);
+    for (size_t u = 0; u < M; ++u)
+      for (size_t t = 0; t < T; ++t) {
+        const float e = E[u * T + t];
+        const float* wr = &m.W[(size_t)in_id[u] * d];
+        const float* cr = &m.C[(size_t)out_id[t] * d];
+        for (int k = 0; k < d; ++k) {
+          dW[u * d + k] += e * cr[k];
+          dC[t * d + k] += e * wr[k];
+        }
+      }
+    for (size_t u = 0; u < M; ++u)
+      for (int k = 0; k < d; ++k) m.W[(size_t)in_id[u] * d + k] += dW[u * d + k];
+    for (size_t t = 0; t < T; ++t)
+      for (int k = 0; k < d; ++k) m.C[(size_t)out_id[t] * d + k] += dC[t * d + k];
+  }
+}
+
 // alpha schedule (Word2Vec.cpp:379-380)
 inline float schedule(const Orc& m, int64_t cw) {
   return std::max(m.cfg.min_alpha,
@@ -461,7 +534,8 @@ void run_epoch(Orc& m, const int64_t* order, D& dr, int64_t epoch, const int64_t
     if (replay_off) dr.rebase(replay_base + replay_off[epoch * n + s]);
     const int32_t* sent = m.ids.data() + m.off[s];
     const int len = (int)(m.off[s + 1] - m.off[s]);
-    if (m.cfg.cbow) cbow_sentence(m, sent, len, alpha, dr, s);
+    if (m.shared_negatives) sgsn_sentence(m, sent, len, alpha, dr, s);
+    else if (m.cfg.cbow) cbow_sentence(m, sent, len, alpha, dr, s);
     else sg_sentence(m, sent, len, alpha, dr, s);
     m.current_words += len;
   }
@@ -628,6 +702,9 @@ void orc_train_philox(void* h, int32_t epoch0, int32_t epochs, const int64_t* or
   }
 }
 
+// Shared-negatives minibatch skip-gram (sgsn_sentence) for every later training call.
+void orc_set_shared_negatives(void* h, int32_t on) { H(h)->shared_negatives = on != 0; }
+
 void orc_philox(const uint32_t* ctr, uint64_t key, uint32_t* out) {
   philox4x32_10(ctr, (uint32_t)key, (uint32_t)(key >> 32), out);
 }
@@ -670,7 +747,8 @@ int64_t orc_train_omp(void* h, int32_t threads, int64_t n_sent_limit, uint32_t s
       a_now = alpha;
       const int32_t* sent = m.ids.data() + m.off[i];
       const int len = (int)(m.off[i + 1] - m.off[i]);
-      if (m.cfg.cbow) cbow_sentence(m, sent, len, a_now, dr, i);
+      if (m.shared_negatives) sgsn_sentence(m, sent, len, a_now, dr, i);
+      else if (m.cfg.cbow) cbow_sentence(m, sent, len, a_now, dr, i);
       else sg_sentence(m, sent, len, a_now, dr, i);
 #pragma omp atomic
       cw += len;

@@ -19,6 +19,8 @@ W2V_RNG_PHILOX = 0
 W2V_RNG_REPLAY = 1
 W2V_SCHED_PARALLEL = 0
 W2V_SCHED_SEQUENTIAL = 1
+W2V_UPDATE_PER_PAIR = 0
+W2V_UPDATE_SHARED_NEGATIVES = 1
 
 
 class DevConfig(C.Structure):
@@ -88,6 +90,7 @@ SIGNATURES = {
     "w2v_dev_set_private_rows": (C.c_int, [_P, _I32]),
     "w2v_dev_set_private_sync": (C.c_int, [_P, _I32, _F]),
     "w2v_dev_set_max_waves": (C.c_int, [_P, _I64]),
+    "w2v_dev_set_update": (C.c_int, [_P, _I32]),
     "w2v_dev_apply_rows": (C.c_int, [_P, _P, _P, _I32, _P, _P, _F, _I32]),
 }
 

@@ -13,6 +13,7 @@
 #include "w2v_dev.h"
 #include "w2v_kernels.hpp"
 #include "w2v_launch.hpp"
+#include "w2v_shared.hpp"
 
 namespace w2v {
 
@@ -96,6 +97,7 @@ struct w2v_dev {
   int32_t rng = W2V_RNG_PHILOX;
   uint64_t seed = 0;
   int32_t sched = W2V_SCHED_PARALLEL;
+  int32_t update = W2V_UPDATE_PER_PAIR;
   int n_cu = 256;
   bool model_ready = false, vocab_ready = false, corpus_ready = false;
   bool model_bound = false;  // W/C/S owned by the caller
@@ -195,7 +197,7 @@ int w2v_dev_create(const w2v_dev_config* cfg, w2v_dev** out) {
   h->own_stream = true;
   h->n_cu = ncu > 0 ? ncu : 256;
   h->d4 = (cfg->word_dim + 3) & ~3;
-  h->pitch = (cfg->word_dim + 31) & ~31;
+  h->pitch = (cfg->word_dim + 63) & ~63;
   h->nv = pick_nv(cfg->word_dim);
   h->need_C = cfg->negative > 0 || cfg->cbow;
   h->need_S = cfg->hs != 0;
@@ -259,7 +261,7 @@ int w2v_dev_upload_vocab(w2v_dev* h, int64_t V, const float* keep, const int64_t
     if (!h->model_bound) { dfree(h->W); dfree(h->C); dfree(h->S); }
     h->W = h->C = h->S = nullptr;
     h->model_bound = false;
-    h->pitch = (h->cfg.word_dim + 31) & ~31;
+    h->pitch = (h->cfg.word_dim + 63) & ~63;
     h->model_ready = false;
   }
   h->V = V;
@@ -461,6 +463,18 @@ int w2v_dev_get_progress(w2v_dev* h, int64_t* cw) {
 
 static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int64_t count);
 
+// The shared-negatives minibatch covers skip-gram NS only: a 16 x 16 MFMA tile
+// holds <= 16 unique context rows (2 * window <= 16) and the center + <= 15
+// negatives; its draws are Philox (the reference has no such path to replay).
+static int check_shared_negatives(const w2v_dev* h, bool at_launch) {
+  if (h->cfg.cbow || h->cfg.hs || h->cfg.negative <= 0)
+    return fail(W2V_ERR_UNSUPPORTED, "shared negatives: skip-gram with negative sampling only (no hs, no cbow)");
+  if (h->cfg.negative > 15) return fail(W2V_ERR_UNSUPPORTED, "shared negatives: negative must be <= 15");
+  if (h->cfg.window > 8) return fail(W2V_ERR_UNSUPPORTED, "shared negatives: window must be <= 8");
+  if (at_launch && h->rng != W2V_RNG_PHILOX) return fail(W2V_ERR_UNSUPPORTED, "shared negatives: Philox draws only");
+  return W2V_OK;
+}
+
 int w2v_dev_train_epoch_async(w2v_dev* h, int32_t epoch, const int64_t* order_dev) {
   if (!h) return fail(W2V_ERR_ARG, "null handle");
   return launch_train(h, epoch, order_dev, h->n_sent);
@@ -483,6 +497,12 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
       return fail(W2V_ERR_ARG, "replay offsets do not cover this epoch");
   }
   if (epoch < 0) return fail(W2V_ERR_ARG, "epoch must be >= 0");
+  KernelFn sn_fn = nullptr;
+  if (h->update == W2V_UPDATE_SHARED_NEGATIVES) {
+    if (int rc = check_shared_negatives(h, true)) return rc;
+    if (h->pitch % 64 != 0 || !(sn_fn = w2v::pick_shared_neg((int)(h->pitch / 64))))
+      return fail(W2V_ERR_UNSUPPORTED, "shared negatives: row pitch must be 64 * {1..8,10,12,16} floats");
+  }
   if (count == 0) return W2V_OK;
   if (set_device(h)) return W2V_ERR_HIP;
   w2v::TrainArgs a;
@@ -545,6 +565,23 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
       a.priv_n = (int32_t)P;
       lds_bytes = (size_t)(P * row_bytes) + 16 + (size_t)P * 4;  // + mask, counts, per-row hits
     }
+  }
+  if (sn_fn) {  // shared-negatives minibatch: 4-wave workgroups, static LDS, no privatisation
+    a.priv_M = nullptr;
+    a.priv_n = 0;
+    HIP_TRY(hipMemsetAsync(h->work, 0, sizeof(unsigned int), h->stream));
+    const int threads = w2v::kSnWaves * w2v::kWave;
+    int64_t g = 1;
+    if (h->sched == W2V_SCHED_PARALLEL) {
+      int per_cu = 0;
+      HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sn_fn, threads, 0));
+      if (per_cu < 1) per_cu = 1;
+      g = std::min<int64_t>((int64_t)per_cu * h->n_cu, count);
+      if (h->max_waves > 0) g = std::max<int64_t>(1, std::min<int64_t>(g, h->max_waves / w2v::kSnWaves));
+    }
+    hipLaunchKernelGGL(sn_fn, dim3((unsigned)g), dim3(threads), 0, h->stream, a);
+    HIP_TRY(hipGetLastError());
+    return W2V_OK;
   }
   KernelFn fn = kernel_for(h);
   HIP_TRY(hipMemsetAsync(h->work, 0, sizeof(unsigned int), h->stream));
@@ -652,6 +689,15 @@ int w2v_dev_set_private_sync(w2v_dev* h, int32_t flush_centers, float average_ov
   if (!(average_over >= 0.0f)) return fail(W2V_ERR_ARG, "average_over must be >= 0");
   h->flush_centers = flush_centers;
   h->private_average = average_over;
+  return W2V_OK;
+}
+
+int w2v_dev_set_update(w2v_dev* h, int32_t mode) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (mode != W2V_UPDATE_PER_PAIR && mode != W2V_UPDATE_SHARED_NEGATIVES) return fail(W2V_ERR_ARG, "bad update mode");
+  if (mode == W2V_UPDATE_SHARED_NEGATIVES)
+    if (int rc = check_shared_negatives(h, false)) return rc;
+  h->update = mode;
   return W2V_OK;
 }
 

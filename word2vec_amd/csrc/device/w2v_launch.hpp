@@ -22,4 +22,8 @@ W2V_DECLARE_NV(12)
 W2V_DECLARE_NV(16)
 #undef W2V_DECLARE_NV
 
+// Shared-negatives minibatch SG (w2v_shared.hip): row pitch = 64 * kb floats;
+// null for a pitch without an instantiation.
+KernelFn pick_shared_neg(int kb);
+
 }  // namespace w2v

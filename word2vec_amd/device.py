@@ -190,6 +190,11 @@ class DeviceTrainer:
         """Cap on wavefronts in flight (0 = as many as fit)."""
         self._chk(self.lib.w2v_dev_set_max_waves(self.h, int(n)), "w2v_dev_set_max_waves")
 
+    def set_update(self, mode: int):
+        """W2V_UPDATE_PER_PAIR (the reference's, default) or W2V_UPDATE_SHARED_NEGATIVES
+        (minibatch skip-gram on the matrix cores, BASELINE configs[4]); include/w2v_dev.h."""
+        self._chk(self.lib.w2v_dev_set_update(self.h, int(mode)), "w2v_dev_set_update")
+
     def set_fixed_alpha(self, alpha: float):
         self._chk(self.lib.w2v_dev_set_fixed_alpha(self.h, float(alpha)), "w2v_dev_set_fixed_alpha")
 
