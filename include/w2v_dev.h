@@ -16,8 +16,8 @@
  *
  * Device layout (HBM): W, C and synapses1 are row-major fp32 with a row pitch
  * of round_up(word_dim, 64) floats (256-B aligned rows; a per-pair kernel lane
- * owns elements lane + 64 v of a row, the shared-negatives kernel's wave w the
- * columns [pitch/4 w, pitch/4 (w+1))); the unigram table is
+ * owns elements lane + 64 v of a row, the shared-negatives kernel's wave w of
+ * n the columns [pitch/n w, pitch/n (w+1))); the unigram table is
  * uint32[table_size]; sample probabilities fp32[V]; Huffman paths are CSR
  * (uint8 codes, int32 points, int64 offsets); the corpus is int32 token ids
  * with int64 sentence offsets.
@@ -192,7 +192,7 @@ int w2v_dev_set_max_waves(w2v_dev* h, int64_t n);
  * the center plus `negative` draws shared by the whole window the outputs (C
  * rows), and the window's updates are the three GEMMs L = W_in C_out^T,
  * dW_in = E C_out, dC_out = E^T W_in on the matrix cores. Skip-gram NS only,
- * negative <= 15, window <= 8, Philox draws, row pitch 64 * {1..8,10,12,16}
+ * negative <= 15, window <= 8, Philox draws, row pitch 64 * {1..8,10,12,14,16}
  * floats (W2V_ERR_UNSUPPORTED otherwise). */
 int w2v_dev_set_update(w2v_dev* h, int32_t mode);
 

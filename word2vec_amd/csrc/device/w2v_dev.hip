@@ -498,10 +498,13 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   }
   if (epoch < 0) return fail(W2V_ERR_ARG, "epoch must be >= 0");
   KernelFn sn_fn = nullptr;
+  int sn_waves = 0;
   if (h->update == W2V_UPDATE_SHARED_NEGATIVES) {
     if (int rc = check_shared_negatives(h, true)) return rc;
-    if (h->pitch % 64 != 0 || !(sn_fn = w2v::pick_shared_neg((int)(h->pitch / 64))))
-      return fail(W2V_ERR_UNSUPPORTED, "shared negatives: row pitch must be 64 * {1..8,10,12,16} floats");
+    int occ = 0;  // register budget (waves per SIMD); experiment knob
+    if (const char* e = std::getenv("W2V_SN_OCC")) occ = std::atoi(e);
+    if (!(sn_fn = w2v::pick_shared_neg(h->pitch, occ, &sn_waves)))
+      return fail(W2V_ERR_UNSUPPORTED, "shared negatives: row pitch must be 64 * {1..8,10,12,14,16} floats");
   }
   if (count == 0) return W2V_OK;
   if (set_device(h)) return W2V_ERR_HIP;
@@ -570,14 +573,14 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     a.priv_M = nullptr;
     a.priv_n = 0;
     HIP_TRY(hipMemsetAsync(h->work, 0, sizeof(unsigned int), h->stream));
-    const int threads = w2v::kSnWaves * w2v::kWave;
+    const int threads = sn_waves * w2v::kWave;
     int64_t g = 1;
     if (h->sched == W2V_SCHED_PARALLEL) {
       int per_cu = 0;
       HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sn_fn, threads, 0));
       if (per_cu < 1) per_cu = 1;
       g = std::min<int64_t>((int64_t)per_cu * h->n_cu, count);
-      if (h->max_waves > 0) g = std::max<int64_t>(1, std::min<int64_t>(g, h->max_waves / w2v::kSnWaves));
+      if (h->max_waves > 0) g = std::max<int64_t>(1, std::min<int64_t>(g, h->max_waves / sn_waves));
     }
     hipLaunchKernelGGL(sn_fn, dim3((unsigned)g), dim3(threads), 0, h->stream, a);
     HIP_TRY(hipGetLastError());

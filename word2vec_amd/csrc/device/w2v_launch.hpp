@@ -22,8 +22,10 @@ W2V_DECLARE_NV(12)
 W2V_DECLARE_NV(16)
 #undef W2V_DECLARE_NV
 
-// Shared-negatives minibatch SG (w2v_shared.hip): row pitch = 64 * kb floats;
-// null for a pitch without an instantiation.
-KernelFn pick_shared_neg(int kb);
+// Shared-negatives minibatch SG (w2v_shared.hip) for a row pitch (floats, a
+// multiple of 64 up to 1024, not 576/704/832/960); *waves = wavefronts per
+// workgroup; occ = register budget in waves per SIMD (3; else the
+// compiler's choice). Null for a pitch without an instantiation.
+KernelFn pick_shared_neg(int64_t pitch, int occ, int* waves);
 
 }  // namespace w2v

@@ -1,23 +1,35 @@
-// Instantiations of the shared-negatives minibatch kernel (w2v_shared.hpp),
-// one per row pitch of 64 KB floats; w2v_dev.hip dispatches.
+// Instantiations of the shared-negatives minibatch kernel (w2v_shared.hpp):
+// the row pitch decides the waves per center (2 up to 512 floats, 4 beyond)
+// and the 16-column blocks per wave; w2v_dev.hip dispatches.
 #include "w2v_launch.hpp"
 #include "w2v_shared.hpp"
 
 namespace w2v {
 
-KernelFn pick_shared_neg(int kb) {
-  switch (kb) {
-    case 1: return &train_shared_neg_kernel<1>;
-    case 2: return &train_shared_neg_kernel<2>;
-    case 3: return &train_shared_neg_kernel<3>;
-    case 4: return &train_shared_neg_kernel<4>;
-    case 5: return &train_shared_neg_kernel<5>;
-    case 6: return &train_shared_neg_kernel<6>;
-    case 7: return &train_shared_neg_kernel<7>;
-    case 8: return &train_shared_neg_kernel<8>;
-    case 10: return &train_shared_neg_kernel<10>;
-    case 12: return &train_shared_neg_kernel<12>;
-    case 16: return &train_shared_neg_kernel<16>;
+template <int KB, int NW>
+static KernelFn pick_occ(int occ) {
+  switch (occ) {
+    case 3: return &train_shared_neg_kernel<KB, NW, 3>;
+    default: return &train_shared_neg_kernel<KB, NW, 1>;
+  }
+}
+
+KernelFn pick_shared_neg(int64_t pitch, int occ, int* waves) {
+  if (pitch % 64 != 0) return nullptr;
+  *waves = pitch <= 512 ? 2 : 4;
+  switch (pitch / 64) {
+    case 1: return pick_occ<2, 2>(occ);
+    case 2: return pick_occ<4, 2>(occ);
+    case 3: return pick_occ<6, 2>(occ);
+    case 4: return pick_occ<8, 2>(occ);
+    case 5: return pick_occ<10, 2>(occ);
+    case 6: return pick_occ<12, 2>(occ);
+    case 7: return pick_occ<14, 2>(occ);
+    case 8: return pick_occ<16, 2>(occ);
+    case 10: return pick_occ<10, 4>(occ);
+    case 12: return pick_occ<12, 4>(occ);
+    case 14: return pick_occ<14, 4>(occ);
+    case 16: return pick_occ<16, 4>(occ);
     default: return nullptr;
   }
 }

@@ -13,21 +13,32 @@
 // three small dense GEMMs — the only place in the hot path where MFMA pays.
 //
 // How it maps to MI355X:
-//   * one workgroup of 4 wavefronts per center; wave w owns the column slice
-//     [16 KB w, 16 KB (w + 1)) of every row (KB 16-column blocks). All four
-//     walk the same sentence with identical (Philox) decisions.
+//   * one workgroup of NW wavefronts per center; wave w owns the column slice
+//     [16 KB w, 16 KB (w + 1)) of every row (KB 16-column blocks, NW * KB * 16
+//     = the row pitch). All NW walk the same sentence with identical (Philox)
+//     decisions. Two waves per center keep the per-center bookkeeping
+//     (window dedup, draws) from being repeated on every SIMD while letting
+//     four workgroups (four centers' gathers) share a CU.
 //   * v_mfma_f32_16x16x4_f32 (exact f32 products, f32 accumulation): 16 rows
 //     of W_in and 16 rows of C_out fit one tile, neg 15 + the center = 16.
 //     Rows are gathered straight into the A/B fragment layout: lane (col =
 //     lane & 15, q = lane >> 4) holds row `col`, columns 16 kb + 4q .. +3 (one
 //     16-B load per block; 16 rows x 64 contiguous B per wave instruction).
-//   * L: 4 MFMAs per block; the four waves' partial L tiles meet in LDS (one
-//     barrier per center, double-buffered).
+//     Unused slots point at slot 0's row (same addresses as lane col 0: no
+//     extra traffic), so no load sits behind a branch; E masks them out.
+//   * L: 4 MFMAs per block; the waves' partial L tiles meet in LDS (one
+//     barrier per center, double-buffered). E = f(L) is evaluated once per
+//     element and transposed through LDS.
 //   * dW^T = C^T E^T and dC^T = W^T E come out of the MFMA directly in the
 //     gather layout (so the update is a register add and the write-back the
 //     same 16-B stores as the gather); their A operands need the rows with
 //     the column index on lane & 15, produced per block by a 16x16 transpose
-//     through 2.5 KiB of per-wave LDS (row stride 20 floats: conflict-free).
+//     through double-buffered per-wave LDS (row stride 20 floats:
+//     conflict-free reads).
+//   * latency: per 64-token block of the sentence, each wave stages the
+//     block's token ids (with window margins) and the unigram-table draws of
+//     every kept position (dependent random HBM reads) in LDS with one wait;
+//     a center then issues no memory operation before its row gathers.
 //   * Hogwild across workgroups (plain read-modify-write stores), exactly as
 //     the per-pair kernel's default class of rows.
 #pragma once
@@ -37,15 +48,32 @@ namespace w2v {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kSnWaves = 4;     // wavefronts per workgroup (column slices)
 constexpr int kSnTile = 16;     // MFMA tile edge: context rows, output rows
 constexpr int kSnStride = 20;   // transpose block row stride in floats
 
+template <int NW>
 struct SnShared {
-  f32x4 part[2][kSnWaves][kWave];                // partial L tiles, by center parity
-  float tr[kSnWaves][2][kSnTile * kSnStride];    // per-wave transpose blocks (W, C)
+  f32x4 part[2][NW][kWave];                      // partial L tiles, by center parity
+  f32x4 e[NW][kWave];                            // per-wave E tile (for its transpose)
+  float tr[NW][2][2][kSnTile * kSnStride];       // per-wave transpose blocks [buffer][W, C]
+  int win[NW][2 * kWave];                        // per-wave block ids: positions i0 - 8 .. i0 + 119
+  int draw[NW][kWave][kSnTile];                  // per-wave draws: [position in block][k]
   uint32_t item[2];                              // dequeued work item, by sentence parity
   float alpha[2];
+};
+
+// Phase timing (diagnostic builds only: make prof, -DW2V_SN_PROF=1; tools/sn_prof.sh).
+struct SnProf {
+#ifdef W2V_SN_PROF
+  unsigned long long t = 0, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  __device__ void stamp(int k) {
+    const unsigned long long now = __builtin_amdgcn_s_memtime();
+    acc[k] += now - t;
+    t = now;
+  }
+#else
+  __device__ void stamp(int) {}
+#endif
 };
 
 __device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
@@ -64,28 +92,31 @@ __device__ __forceinline__ float sn_grad(float l, bool positive, float alpha) {
   return ((positive ? 1.0f : 0.0f) - f) * alpha;
 }
 
-template <int KB>
-__device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared& sh, int wave, int lane,
-                                          const int32_t* sent, int len, int i, int c, int rw, uint32_t s,
-                                          float alpha, int& par, Counters& cnt) {
+constexpr int kSnMargin = 8;  // window <= 8: ids of positions [i0 - 8, i0 + 72) cover every window of a block
+
+template <int KB, int NW>
+__device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<NW>& sh, int wave, int lane, int len, int i0,
+                                          int b, int c, int rw, float alpha, int& par, Counters& cnt, SnProf& pf_) {
+  pf_.stamp(0);
   const int q = lane >> 4, col = lane & 15;
+  const int i = i0 + b;
   const int lo = max(0, i - a.window + rw), hi = min(len, i + a.window + 1 - rw);
-  const int span = hi - lo, me = i - lo;
-  const bool valid = lane < span && lane != me;
-  const int id = valid ? sent[lo + lane] : -1;
+  const int span = hi - lo;
+  const int wv = sh.win[wave][min(lo - (i0 - kSnMargin) + lane, 2 * kWave - 1)];
+  const int id = (lane < span && lo + lane != i) ? wv : -1;
   // unique context ids (first occurrence) and their multiplicities
-  bool dup = !valid;
+  bool dup = id < 0;
   int mult = 0;
   for (int j = 0; j < span; ++j) {
     const int v = readlane_i(id, j);
-    if (j != me && v == id) {
+    if (v == id) {
       mult += 1;
       dup = dup || (j < lane);
     }
   }
   const unsigned long long uniq = ballot(!dup);
   const int M = __popcll(uniq);
-  if (M == 0) return;  // workgroup-uniform
+  if (M == 0) return;  // workgroup-uniform (a one-token sentence)
   int in_l = 0, m_l = 0;
   {
     unsigned long long m = uniq;
@@ -96,11 +127,18 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared& sh, int 
       if (lane == t) { in_l = v; m_l = mm; }
     }
   }
+  // W row gathers (slot col, or slot 0's row for an unused slot)
+  const bool in_ok = col < M;
+  const int in_row = __shfl(in_l, in_ok ? col : 0);
+  const int64_t cb = (int64_t)wave * (kSnTile * KB) + 4 * q;
+  float* wp = a.W + (int64_t)in_row * a.pitch + cb;
+  if (a.strict) drain_vmem();  // sequential schedule: this wave's own stores land before the re-read
+  f32x4 wr[KB], cr[KB];
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) wr[kb] = *reinterpret_cast<const f32x4*>(wp + kSnTile * kb);
   // outputs: lane 0 the center, lane t in [1, K] the (t-1)-th shared draw
   const int K = a.negative;
-  int neg_l = 0;
-  if (lane < K) neg_l = (int)a.table[philox_table_pos(a, s, (uint32_t)i, 0u, (uint32_t)lane)];
-  const int prev_draw = __shfl(neg_l, (lane + kWave - 1) & (kWave - 1));  // every lane takes part
+  const int prev_draw = sh.draw[wave][b][(lane + kSnTile - 1) & (kSnTile - 1)];
   const int out_l = (lane == 0) ? c : prev_draw;
   bool ok = (lane == 0) || (lane <= K && out_l != c);
   for (int j = 1; j < K; ++j) {
@@ -108,26 +146,22 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared& sh, int 
     ok = ok && !(j < lane && v == out_l);
   }
   const unsigned long long okm = ballot(ok);
+  const bool out_ok = (okm >> col) & 1ull;
+  const int out_row = __shfl(out_l, out_ok ? col : 0);
+  float* cp = a.C + (int64_t)out_row * a.pitch + cb;
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) cr[kb] = *reinterpret_cast<const f32x4*>(cp + kSnTile * kb);
   cnt.centers += 1;
   cnt.contexts += (unsigned long long)M;
   cnt.targets += (unsigned long long)__popcll(okm);
   cnt.draws += (unsigned long long)K;
-
-  // gathers into the fragment layout
-  const int in_row = __shfl(in_l, col), out_row = __shfl(out_l, col);
-  const bool in_ok = col < M, out_ok = (okm >> col) & 1ull;
-  const int64_t cb = (int64_t)wave * (kSnTile * KB) + 4 * q;
-  float* wp = a.W + (int64_t)in_row * a.pitch + cb;
-  float* cp = a.C + (int64_t)out_row * a.pitch + cb;
-  if (a.strict) drain_vmem();  // sequential schedule: this wave's own stores land before the re-read
-  f32x4 wr[KB], cr[KB];
-#pragma unroll
-  for (int kb = 0; kb < KB; ++kb) {
-    wr[kb] = in_ok ? *reinterpret_cast<const f32x4*>(wp + kSnTile * kb) : f32x4{0.f, 0.f, 0.f, 0.f};
-    cr[kb] = out_ok ? *reinterpret_cast<const f32x4*>(cp + kSnTile * kb) : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
+  pf_.stamp(1);
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  // unused slots hold slot 0's row: finite, and every E term that touches them
+  // is masked to zero below, so they add nothing to dW, dC (and are not stored)
+  pf_.stamp(2);
   // L (this wave's column slice), then the workgroup sum
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f32x4 acc = zero;
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) {
     acc = mfma16x16x4(wr[kb][0], cr[kb][0], acc);
@@ -136,73 +170,83 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared& sh, int 
     acc = mfma16x16x4(wr[kb][3], cr[kb][3], acc);
   }
   sh.part[par][wave][lane] = acc;
+  pf_.stamp(3);
   __syncthreads();
-  // lane holds L[4q + r][col]; Lt[s] = L[col][4q + s] (same sums, same order)
+  pf_.stamp(4);
+  // lane holds L[4q + r][col] (the partials summed in wave order: the same
+  // value in every wave); E once per element, Et[s] = E[col][4q + s] by LDS
   f32x4 L = sh.part[par][0][lane];
 #pragma unroll
-  for (int w = 1; w < kSnWaves; ++w) L += sh.part[par][w][lane];
-  float Lt[4];
-  {
-    const float* pf = reinterpret_cast<const float*>(&sh.part[par][0][0]);
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
-      const int idx = (((col >> 2) * 16 + 4 * q + s4) << 2) + (col & 3);
-      float v = pf[idx];
-#pragma unroll
-      for (int w = 1; w < kSnWaves; ++w) v += pf[w * kWave * 4 + idx];
-      Lt[s4] = v;
-    }
-  }
+  for (int w = 1; w < NW; ++w) L += sh.part[par][w][lane];
   par ^= 1;
-  // E in both layouts: Ea[r] = E[4q + r][col], Et[s] = E[col][4q + s]
-  float Ea[4], Et[4];
-  const int m_col = __shfl(m_l, col);
+  f32x4 Ea;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int u = 4 * q + r;
     const int m_u = __shfl(m_l, u);
-    const bool pair_a = u < M && ((okm >> col) & 1ull);
-    Ea[r] = pair_a ? (float)m_u * sn_grad(L[r], col == 0, alpha) : 0.f;
-    const int t = 4 * q + r;
-    const bool pair_t = col < M && ((okm >> t) & 1ull);
-    Et[r] = pair_t ? (float)m_col * sn_grad(Lt[r], t == 0, alpha) : 0.f;
+    Ea[r] = (u < M && out_ok) ? (float)m_u * sn_grad(L[r], col == 0, alpha) : 0.f;
   }
-  // dW^T = C^T E^T and dC^T = W^T E per 16-column block, added in place
-  float* tw = sh.tr[wave][0];
-  float* tc = sh.tr[wave][1];
+  sh.e[wave][lane] = Ea;
+  wave_lds_order();
+  // contraction step s of dW covers outputs 4s + q, of dC inputs 4s + q, so the
+  // steps past the last output (K + 1) or the last input (M) are skipped
+  float Eo[4], Ei[4];
+  {
+    const float* pe = reinterpret_cast<const float*>(&sh.e[wave][0]);
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      Eo[s4] = pe[((((col >> 2) << 4) + 4 * s4 + q) << 2) + (col & 3)];  // E[col][4s + q]
+      Ei[s4] = pe[((col + 16 * s4) << 2) + q];                            // E[4s + q][col]
+    }
+  }
+  const int n_out = (K + 1 + 3) >> 2, n_in = (M + 3) >> 2;
+  pf_.stamp(5);
+  // dW^T = C^T E^T and dC^T = W^T E per 16-column block, added in place;
+  // block kb + 1 goes into the other transpose buffer while kb is consumed
+  float* tb[2][2] = {{sh.tr[wave][0][0], sh.tr[wave][0][1]}, {sh.tr[wave][1][0], sh.tr[wave][1][1]}};
+  *reinterpret_cast<f32x4*>(tb[0][0] + col * kSnStride + 4 * q) = wr[0];
+  *reinterpret_cast<f32x4*>(tb[0][1] + col * kSnStride + 4 * q) = cr[0];
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) {
-    *reinterpret_cast<f32x4*>(tw + col * kSnStride + 4 * q) = wr[kb];
-    *reinterpret_cast<f32x4*>(tc + col * kSnStride + 4 * q) = cr[kb];
     wave_lds_order();
+    const float* tw = tb[kb & 1][0];
+    const float* tc = tb[kb & 1][1];
     float wd[4], cd[4];
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
-      wd[s4] = tw[(4 * q + s4) * kSnStride + col];  // W[4q + s][16 kb + col]
-      cd[s4] = tc[(4 * q + s4) * kSnStride + col];  // C[4q + s][16 kb + col]
+      wd[s4] = tw[(4 * s4 + q) * kSnStride + col];  // W[4s + q][16 kb + col]
+      cd[s4] = tc[(4 * s4 + q) * kSnStride + col];  // C[4s + q][16 kb + col]
     }
-    wave_lds_order();
-    f32x4 dw = {0.f, 0.f, 0.f, 0.f}, dc = {0.f, 0.f, 0.f, 0.f};
+    if (kb + 1 < KB) {
+      *reinterpret_cast<f32x4*>(tb[(kb + 1) & 1][0] + col * kSnStride + 4 * q) = wr[kb + 1];
+      *reinterpret_cast<f32x4*>(tb[(kb + 1) & 1][1] + col * kSnStride + 4 * q) = cr[kb + 1];
+    }
+    f32x4 dw = zero, dc = zero;
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
-      dw = mfma16x16x4(cd[s4], Et[s4], dw);  // dW[col][16 kb + 4q + r]
-      dc = mfma16x16x4(wd[s4], Ea[s4], dc);  // dC[col][16 kb + 4q + r]
+      if (s4 < n_out) dw = mfma16x16x4(cd[s4], Eo[s4], dw);  // dW[col][16 kb + 4q + r]
+      if (s4 < n_in) dc = mfma16x16x4(wd[s4], Ei[s4], dc);   // dC[col][16 kb + 4q + r]
     }
     wr[kb] += dw;
     cr[kb] += dc;
     if (in_ok) *reinterpret_cast<f32x4*>(wp + kSnTile * kb) = wr[kb];
     if (out_ok) *reinterpret_cast<f32x4*>(cp + kSnTile * kb) = cr[kb];
   }
+  pf_.stamp(6);
 }
 
 // Epoch kernel: workgroups dequeue sentences (Word2Vec.cpp:375-394) and walk
 // them with the reference's subsampling and window shrink (Philox draws).
-template <int KB>
-__global__ __launch_bounds__(kSnWaves * kWave) void train_shared_neg_kernel(TrainArgs a) {
-  __shared__ SnShared sh;
+template <int KB, int NW, int WAVES_PER_SIMD>
+__global__ __launch_bounds__(NW * kWave, WAVES_PER_SIMD) void train_shared_neg_kernel(TrainArgs a) {
+  __shared__ SnShared<NW> sh;
   const int lane = lane_id();
   const int wave = (int)(threadIdx.x >> 6);
   Counters cnt;
+  SnProf prof;
+#ifdef W2V_SN_PROF
+  prof.t = __builtin_amdgcn_s_memtime();
+#endif
   int par = 0;
   float alpha0 = a.init_alpha;  // thread 0's schedule state
   bool first = true;
@@ -242,17 +286,44 @@ __global__ __launch_bounds__(kSnWaves * kWave) void train_shared_neg_kernel(Trai
       philox((uint32_t)ii, (uint32_t)s, 0xFFFFFFFFu, a.epoch, a.key0, a.key1, o0, o1, o2, o3);
       const float u_l = canonical_f(o0);
       const int rw_l = (int)(((uint64_t)o1 * wmax) >> 32);
-      unsigned long long kept = ballot(in && !(p_l < u_l));
+      const bool keep_l = in && !(p_l < u_l);
+      unsigned long long kept = ballot(keep_l);
+      if (!kept) continue;
+      // stage the block's ids (with margins) and every kept position's draws
+      {
+        const int ja = min(max(i0 - kSnMargin + lane, 0), len - 1), jb = min(i0 - kSnMargin + kWave + lane, len - 1);
+        const int va = sent[ja], vb = sent[jb];
+        int dv[kSnTile];
+#pragma unroll
+        for (int kk = 0; kk < kSnTile; ++kk) {
+          dv[kk] = 0;
+          if (keep_l && kk < a.negative)
+            dv[kk] = (int)a.table[philox_table_pos(a, (uint32_t)s, (uint32_t)ii, 0u, (uint32_t)kk)];
+        }
+        sh.win[wave][lane] = va;
+        sh.win[wave][kWave + lane] = vb;
+#pragma unroll
+        for (int kk = 0; kk < kSnTile; kk += 4)
+          *reinterpret_cast<int4*>(&sh.draw[wave][lane][kk]) = make_int4(dv[kk], dv[kk + 1], dv[kk + 2], dv[kk + 3]);
+        wave_lds_order();
+      }
       while (kept) {
         const int b = __builtin_ctzll(kept);
         kept &= kept - 1;
-        sn_center<KB>(a, sh, wave, lane, sent, len, i0 + b, readlane_i(c_l, b), readlane_i(rw_l, b), (uint32_t)s,
-                      alpha, par, cnt);
+        sn_center<KB, NW>(a, sh, wave, lane, len, i0, b, readlane_i(c_l, b), readlane_i(rw_l, b), alpha, par, cnt,
+                          prof);
       }
     }
     if (threadIdx.x == 0) atomicAdd(a.words, (unsigned long long)len);
     cnt.sentences += 1;
   }
+#ifdef W2V_SN_PROF
+  prof.stamp(0);
+  if (lane == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))
+    printf("SNPROF block %u wave %d centers %llu sent %llu: %llu %llu %llu %llu %llu %llu %llu\n", blockIdx.x, wave,
+           cnt.centers, cnt.sentences, prof.acc[0], prof.acc[1], prof.acc[2], prof.acc[3], prof.acc[4], prof.acc[5],
+           prof.acc[6]);
+#endif
   if (threadIdx.x == 0) {  // every wave counted the same centers; wave 0 reports
     atomicAdd(&a.stats[0], cnt.centers);
     atomicAdd(&a.stats[1], cnt.contexts);

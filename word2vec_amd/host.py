@@ -4,11 +4,14 @@ reference's make_table / precalc_sampling / create_huffman_tree)."""
 from __future__ import annotations
 
 import ctypes as C
+import os
 from pathlib import Path
 
 import numpy as np
 
 HOST_LIB = Path(__file__).resolve().parent / "lib" / "libword2vec_amd.so"
+if os.environ.get("W2V_DEV_LIB"):  # a diagnostic device library: use the host library linked beside it
+    HOST_LIB = Path(os.environ["W2V_DEV_LIB"]).resolve().parent / "libword2vec_amd.so"
 _lib = None
 
 
