@@ -28,6 +28,8 @@ void w2v_model_options(w2v_model* m, int32_t gpu_device, int32_t replay_rng, int
 /* Parallel-schedule update policy (Word2Vec.h additive members; include/w2v_dev.h). */
 void w2v_model_update_policy(w2v_model* m, int64_t hot_rows, int32_t private_rows, int32_t flush_centers,
                              float private_average, int64_t max_waves);
+/* Word2Vec::shared_negatives (configs[4] minibatch skip-gram; include/w2v_dev.h w2v_dev_set_update). */
+void w2v_model_set_shared_negatives(w2v_model* m, int32_t on);
 
 /* Sentences as text: one per line, whitespace-separated tokens (line_docs format). */
 int w2v_model_build_vocab(w2v_model* m, const char* text, int64_t len);

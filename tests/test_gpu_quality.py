@@ -63,3 +63,32 @@ def test_quality_text8_like_not_below_oracle():
     ref = np.array([[r["analogy"], r["similarity"]] for r in ZGOLD["scores"]]).mean(0)
     print(f"text8-like sg_ns: gpu {got.round(2)} oracle {ref.round(2)} delta {(got - ref).round(2)}")
     assert got[0] >= ref[0] - 1.0 and got[1] >= ref[1] - 1.0
+
+
+@pytest.mark.parametrize("corpus", ["planted", "text8-like"])
+def test_quality_shared_negatives_not_below_oracle(corpus):
+    """configs[4]'s shared-negatives minibatch (no reference counterpart) against
+    the reference's per-pair oracle scores at the same hyperparameters (neg 5)."""
+    def train(sents, iters, dim, table, sub, seed):
+        w = Word2Vec(iter=iters, window=5, min_count=5, table_size=table, word_dim=dim, negative=5,
+                     subsample_threshold=sub, init_alpha=0.025, min_alpha=2.5e-6, cbow_mean=True, train_method="ns",
+                     model="sg", shared_negatives=True, verbose=False)
+        w.seed(seed)
+        w.build_vocab(sents)
+        w.init_weights()
+        w.train(sents)
+        words, _ = w.vocab()
+        return words, w.matrix(0)
+
+    if corpus == "planted":
+        sents, qs, pairs = SENTS, QS, PAIRS
+        args = (ITERS["sg_ns"], TRAIN["dim"], TRAIN["table_size"], TRAIN["subsample"])
+        ref = np.array([[r["analogy"], r["similarity"]] for r in GOLD["scores"]["sg_ns"]]).mean(0)
+    else:
+        sents, qs, pairs = planted_zipf_corpus(**ZCORPUS)
+        args = (ZTRAIN["iters"], ZTRAIN["dim"], ZTRAIN["table_size"], ZTRAIN["subsample"])
+        ref = np.array([[r["analogy"], r["similarity"]] for r in ZGOLD["scores"]]).mean(0)
+    words, E = train(sents, *args, 11)
+    got = np.array([analogy_accuracy(words, E, qs)["accuracy"], similarity_score(words, E, pairs)["spearman"]])
+    print(f"shared-negatives {corpus}: gpu {got.round(2)} oracle(per-pair) {ref.round(2)} delta {(got - ref).round(2)}")
+    assert got[0] >= ref[0] - 1.0 and got[1] >= ref[1] - 1.0

@@ -31,6 +31,7 @@ __global__ void expand_table_kernel(const int64_t* bounds, int64_t V, uint32_t* 
   }
 }
 
+
 }  // namespace w2v
 
 namespace {
@@ -503,12 +504,14 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     if (int rc = check_shared_negatives(h, true)) return rc;
     int occ = 0;  // register budget (waves per SIMD); experiment knob
     if (const char* e = std::getenv("W2V_SN_OCC")) occ = std::atoi(e);
+    if ((double)h->V * (double)h->pitch * sizeof(float) >= 4294967296.0)
+      return fail(W2V_ERR_UNSUPPORTED, "shared negatives: W / C must be < 4 GiB each (32-bit buffer offsets)");
     if (!(sn_fn = w2v::pick_shared_neg(h->pitch, occ, &sn_waves)))
       return fail(W2V_ERR_UNSUPPORTED, "shared negatives: row pitch must be 64 * {1..8,10,12,14,16} floats");
   }
   if (count == 0) return W2V_OK;
   if (set_device(h)) return W2V_ERR_HIP;
-  w2v::TrainArgs a;
+  w2v::TrainArgs a{};
   a.W = h->W; a.C = h->C; a.S = h->S;
   a.pitch = h->pitch; a.dim = h->cfg.word_dim;
   a.window = h->cfg.window; a.negative = h->cfg.negative; a.cbow_mean = h->cfg.cbow_mean;
@@ -569,19 +572,29 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
       lds_bytes = (size_t)(P * row_bytes) + 16 + (size_t)P * 4;  // + mask, counts, per-row hits
     }
   }
-  if (sn_fn) {  // shared-negatives minibatch: 4-wave workgroups, static LDS, no privatisation
+  if (sn_fn) {  // shared-negatives minibatch: 2-wave workgroups, static LDS, no privatisation
     a.priv_M = nullptr;
     a.priv_n = 0;
-    HIP_TRY(hipMemsetAsync(h->work, 0, sizeof(unsigned int), h->stream));
+    a.item0 = 0;
     const int threads = sn_waves * w2v::kWave;
+    // device-coherent rows (rows_rsrc in w2v_shared.hpp): all for hot_rows =
+    // -1, else at least the rows two XCD L2s' capacity could keep resident
+    const int64_t l2_rows = (int64_t)(8 << 20) / (h->pitch * (int64_t)sizeof(float));
+    a.hot_wc = h->hot_rows < 0 ? h->V : std::min<int64_t>(h->V, std::max<int64_t>(h->hot_rows, l2_rows));
     int64_t g = 1;
     if (h->sched == W2V_SCHED_PARALLEL) {
       int per_cu = 0;
       HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sn_fn, threads, 0));
       if (per_cu < 1) per_cu = 1;
+      // Concurrency a vocab can take (measured on the planted corpora: quality
+      // holds at 1 workgroup per CU for V = 3.4K and 2 for V = 98K, and
+      // collapses at 4): every center holds ~22 rows for its whole update, so
+      // a small vocab's frequent rows are held by hundreds of workgroups at once.
+      if (h->max_waves == 0) per_cu = std::min(per_cu, h->V < 16384 ? 1 : h->V < 524288 ? 2 : per_cu);
       g = std::min<int64_t>((int64_t)per_cu * h->n_cu, count);
       if (h->max_waves > 0) g = std::max<int64_t>(1, std::min<int64_t>(g, h->max_waves / sn_waves));
     }
+    HIP_TRY(hipMemsetAsync(h->work, 0, sizeof(unsigned int), h->stream));
     hipLaunchKernelGGL(sn_fn, dim3((unsigned)g), dim3(threads), 0, h->stream, a);
     HIP_TRY(hipGetLastError());
     return W2V_OK;

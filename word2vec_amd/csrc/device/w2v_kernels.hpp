@@ -83,7 +83,7 @@ struct TrainArgs {
   unsigned long long* stats;   // centers, contexts, targets, draws, sentences
   uint32_t key0, key1, epoch;
   float fixed_alpha;           // > 0: use instead of the schedule
-  int64_t hot_wc;              // W / C rows [0, hot_wc) update with atomics
+  int64_t hot_wc;              // W / C rows [0, hot_wc) update with atomics (shared-negatives: sc1 traffic)
   int64_t hot_s;               // synapses1 rows [hot_s, V-1) update with atomics
   int32_t strict;              // 1: drain own atomics before re-reading (sequential schedule)
   const float* priv_M;         // output matrix whose hottest rows are privatised in LDS (or null)
@@ -91,6 +91,7 @@ struct TrainArgs {
   int32_t priv_n;
   float priv_avg;              // > 0: average, not sum, the workgroups' deltas of a privatised row (see flush_private)
   int32_t flush_every;         // the privatised deltas are flushed every this many centers of the workgroup
+  int64_t item0;               // shared-negatives kernel: work items are order[item0 + k] (or item0 + k)
 };
 
 struct Counters {

@@ -39,8 +39,8 @@
 //     block's token ids (with window margins) and the unigram-table draws of
 //     every kept position (dependent random HBM reads) in LDS with one wait;
 //     a center then issues no memory operation before its row gathers.
-//   * Hogwild across workgroups (plain read-modify-write stores), exactly as
-//     the per-pair kernel's default class of rows.
+//   * Hogwild across workgroups (read-modify-write), the frequent rows with
+//     device-coherent (sc1) loads and write-through stores: see rows_rsrc.
 #pragma once
 #include "w2v_kernels.hpp"
 
@@ -80,6 +80,54 @@ __device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// Row traffic of the frequent rows is device-coherent. Per-XCD L2s are not
+// coherent with each other inside a launch (MI355X_MICROARCH.md, XCD): with
+// plain (write-back) stores every XCD keeps training its own L2-resident
+// version of the rows it touches constantly, and the versions are merged line
+// by line at write-back (measured: analogy accuracy collapses to ~0 as soon
+// as workgroups span two XCDs). Rows below a.hot_wc (the vocab is sorted by
+// count: the rows an L2 could keep resident) are loaded with sc1 (skips the
+// CU's L1, which other CUs' stores never refresh) and stored with sc1
+// (write-through: the line leaves the writer's L2), so a copy lives in an L2
+// only between one read and that workgroup's write-back. Rarer rows are
+// evicted from any L2 long before their next use and keep the cached path.
+// Measured alternatives: per-XCD replicas merged between
+// launches diverge (summed deltas) or under-train (averaged).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, -1, 0x00020000);
+}
+constexpr int kSc1 = 16;  // buffer cache-policy bit: sc1 (device scope)
+__device__ __forceinline__ f32x4 load_row4(__amdgpu_buffer_rsrc_t r, uint32_t off, bool coherent) {
+  if (coherent) return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kSc1);
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+__device__ __forceinline__ void store_row4(f32x4 v, __amdgpu_buffer_rsrc_t r, uint32_t off, bool coherent) {
+  if (coherent) __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kSc1);
+  else __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+}
+
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false); }
+
+// Write back two consecutive 16-column blocks (lo = block 2j, hi = block 2j+1,
+// fragment layout: lane (col, q) holds row col, columns 4q..4q+3 of each) as
+// two instructions of 8 rows x 128 contiguous bytes, so that a write-through
+// (sc1) store sends whole lines to memory instead of 64-B halves. Lane col and its partner col ^ 8 (DPP row_ror:8)
+// trade their hi blocks: instruction 0 writes rows 0..7, instruction 1 rows 8..15.
+__device__ __forceinline__ void store_pair(f32x4 lo, f32x4 hi, __amdgpu_buffer_rsrc_t r, uint32_t off, bool ok, bool coh,
+                                           int col) {
+  f32x4 hp;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) hp[e] = __int_as_float(dpp_i<0x128>(__float_as_int(hi[e])));
+  const uint32_t off_p = (uint32_t)dpp_i<0x128>((int)off) + 64u;  // partner row, block 2j+1
+  const bool ok_p = dpp_i<0x128>((int)ok) != 0, coh_p = dpp_i<0x128>((int)coh) != 0;
+  const bool low = col < 8;
+  // instruction 0: rows 0..7 — own lo for col < 8, the partner's hi for col >= 8
+  if (low ? ok : ok_p) store_row4(low ? lo : hp, r, low ? off : off_p, low ? coh : coh_p);
+  // instruction 1: rows 8..15 — own lo for col >= 8, the partner's hi for col < 8
+  if (low ? ok_p : ok) store_row4(low ? hp : lo, r, low ? off_p : off, low ? coh_p : coh);
+}
+
 // Keep this wave's LDS accesses in program order (the LDS unit serves one
 // wave's operations in order; this only stops the compiler reordering them).
 __device__ __forceinline__ void wave_lds_order() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
@@ -95,8 +143,10 @@ __device__ __forceinline__ float sn_grad(float l, bool positive, float alpha) {
 constexpr int kSnMargin = 8;  // window <= 8: ids of positions [i0 - 8, i0 + 72) cover every window of a block
 
 template <int KB, int NW>
-__device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<NW>& sh, int wave, int lane, int len, int i0,
-                                          int b, int c, int rw, float alpha, int& par, Counters& cnt, SnProf& pf_) {
+__device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<NW>& sh, __amdgpu_buffer_rsrc_t rW,
+                                          __amdgpu_buffer_rsrc_t rC,
+                                          int wave, int lane, int len, int i0, int b, int c, int rw, float alpha,
+                                          int& par, Counters& cnt, SnProf& pf_) {
   pf_.stamp(0);
   const int q = lane >> 4, col = lane & 15;
   const int i = i0 + b;
@@ -131,11 +181,12 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<NW>& sh, 
   const bool in_ok = col < M;
   const int in_row = __shfl(in_l, in_ok ? col : 0);
   const int64_t cb = (int64_t)wave * (kSnTile * KB) + 4 * q;
-  float* wp = a.W + (int64_t)in_row * a.pitch + cb;
+  const uint32_t wo = (uint32_t)(((int64_t)in_row * a.pitch + cb) * 4);  // byte offsets (< 4 GiB, host-checked)
+  const bool w_coh = in_row < a.hot_wc;
   if (a.strict) drain_vmem();  // sequential schedule: this wave's own stores land before the re-read
   f32x4 wr[KB], cr[KB];
 #pragma unroll
-  for (int kb = 0; kb < KB; ++kb) wr[kb] = *reinterpret_cast<const f32x4*>(wp + kSnTile * kb);
+  for (int kb = 0; kb < KB; ++kb) wr[kb] = load_row4(rW, wo + 64u * kb, w_coh);
   // outputs: lane 0 the center, lane t in [1, K] the (t-1)-th shared draw
   const int K = a.negative;
   const int prev_draw = sh.draw[wave][b][(lane + kSnTile - 1) & (kSnTile - 1)];
@@ -148,9 +199,10 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<NW>& sh, 
   const unsigned long long okm = ballot(ok);
   const bool out_ok = (okm >> col) & 1ull;
   const int out_row = __shfl(out_l, out_ok ? col : 0);
-  float* cp = a.C + (int64_t)out_row * a.pitch + cb;
+  const uint32_t co = (uint32_t)(((int64_t)out_row * a.pitch + cb) * 4);
+  const bool c_coh = out_row < a.hot_wc;
 #pragma unroll
-  for (int kb = 0; kb < KB; ++kb) cr[kb] = *reinterpret_cast<const f32x4*>(cp + kSnTile * kb);
+  for (int kb = 0; kb < KB; ++kb) cr[kb] = load_row4(rC, co + 64u * kb, c_coh);
   cnt.centers += 1;
   cnt.contexts += (unsigned long long)M;
   cnt.targets += (unsigned long long)__popcll(okm);
@@ -229,8 +281,10 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<NW>& sh, 
     }
     wr[kb] += dw;
     cr[kb] += dc;
-    if (in_ok) *reinterpret_cast<f32x4*>(wp + kSnTile * kb) = wr[kb];
-    if (out_ok) *reinterpret_cast<f32x4*>(cp + kSnTile * kb) = cr[kb];
+    if (kb & 1) {  // blocks kb - 1, kb written back as whole 128-B lines
+      store_pair(wr[kb - 1], wr[kb], rW, wo + 64u * (kb - 1), in_ok, w_coh, col);
+      store_pair(cr[kb - 1], cr[kb], rC, co + 64u * (kb - 1), out_ok, c_coh, col);
+    }
   }
   pf_.stamp(6);
 }
@@ -247,6 +301,7 @@ __global__ __launch_bounds__(NW * kWave, WAVES_PER_SIMD) void train_shared_neg_k
 #ifdef W2V_SN_PROF
   prof.t = __builtin_amdgcn_s_memtime();
 #endif
+  const __amdgpu_buffer_rsrc_t rW = rows_rsrc(a.W), rC = rows_rsrc(a.C);
   int par = 0;
   float alpha0 = a.init_alpha;  // thread 0's schedule state
   bool first = true;
@@ -259,7 +314,7 @@ __global__ __launch_bounds__(NW * kWave, WAVES_PER_SIMD) void train_shared_neg_k
       if ((int64_t)k < a.n_sent) {
         if (a.fixed_alpha > 0.0f) {
           alpha0 = a.fixed_alpha;
-        } else if (first || (k % 10u) == 0u) {
+        } else if (first || ((a.item0 + k) % 10) == 0) {
           const unsigned long long cw = __hip_atomic_load(a.words, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           const float al = (float)(a.init_alpha * (1.0 - 1.0 / a.iter * (double)cw / a.train_words));
           alpha0 = (a.min_alpha < al) ? al : a.min_alpha;
@@ -272,7 +327,7 @@ __global__ __launch_bounds__(NW * kWave, WAVES_PER_SIMD) void train_shared_neg_k
     const uint32_t k = sh.item[slot];
     if ((int64_t)k >= a.n_sent) break;
     const float alpha = sh.alpha[slot];
-    const int64_t s = a.order ? a.order[k] : (int64_t)k;
+    const int64_t s = a.order ? a.order[a.item0 + k] : a.item0 + (int64_t)k;
     if (s < 0 || s >= a.n_corpus) continue;
     const int64_t base = a.soff[s];
     const int len = (int)(a.soff[s + 1] - base);
@@ -310,8 +365,8 @@ __global__ __launch_bounds__(NW * kWave, WAVES_PER_SIMD) void train_shared_neg_k
       while (kept) {
         const int b = __builtin_ctzll(kept);
         kept &= kept - 1;
-        sn_center<KB, NW>(a, sh, wave, lane, len, i0, b, readlane_i(c_l, b), readlane_i(rw_l, b), alpha, par, cnt,
-                          prof);
+        sn_center<KB, NW>(a, sh, rW, rC, wave, lane, len, i0, b, readlane_i(c_l, b), readlane_i(rw_l, b), alpha, par,
+                          cnt, prof);
       }
     }
     if (threadIdx.x == 0) atomicAdd(a.words, (unsigned long long)len);
@@ -334,3 +389,4 @@ __global__ __launch_bounds__(NW * kWave, WAVES_PER_SIMD) void train_shared_neg_k
 }
 
 }  // namespace w2v
+

@@ -6,7 +6,7 @@
 // because cbow_mean is hard-wired true (:117,180-181), min_alpha derived from
 // the pre-override 0.025 (:116), 1000-token sentences (:66), and which matrix
 // is written (:196-201). Additive: -train is honoured (the reference always
-// reads ./text8), -binary, -gpu, -replay.
+// reads ./text8), -binary, -gpu, -replay, -shared-negatives.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -37,7 +37,8 @@ void usage() {
                "  -model <cbow|sg>      architecture (default sg)\n"
                "  -binary <0|1>         write vectors in the binary layout (default 0)\n"
                "  -gpu <int>            HIP device (default 0)\n"
-               "  -replay <0|1>         reference-exact deterministic RNG replay on one wavefront\n\n"
+               "  -replay <0|1>         reference-exact deterministic RNG replay on one wavefront\n"
+               "  -shared-negatives <0|1> skip-gram NS as the shared-negatives minibatch on the matrix cores\n\n"
                "example: ./word2vec -train text8 -output vec.txt -size 300 -window 5 -subsample 1e-4 "
                "-negative 5 -model sg -train_method ns -iter 3\n";
 }
@@ -85,7 +86,7 @@ int main(int argc, char** argv) {
   float init_alpha = 0.025f, subsample_threshold = 0.0001f;
   const float min_alpha = init_alpha * 0.0001;
   const bool cbow_mean = true;
-  int binary = 0, gpu = 0, replay = 0;
+  int binary = 0, gpu = 0, replay = 0, shared = 0;
   int i;
   if ((i = find_flag("-size", argc, argv)) > 0) word_dim = std::atoi(argv[i + 1]);
   if ((i = find_flag("-train", argc, argv)) > 0) input_file = argv[i + 1];
@@ -104,6 +105,7 @@ int main(int argc, char** argv) {
   if ((i = find_flag("-binary", argc, argv)) > 0) binary = std::atoi(argv[i + 1]);
   if ((i = find_flag("-gpu", argc, argv)) > 0) gpu = std::atoi(argv[i + 1]);
   if ((i = find_flag("-replay", argc, argv)) > 0) replay = std::atoi(argv[i + 1]);
+  if ((i = find_flag("-shared-negatives", argc, argv)) > 0) shared = std::atoi(argv[i + 1]);
 
   if (model.empty()) {
     model = "sg";
@@ -131,6 +133,7 @@ int main(int argc, char** argv) {
                min_alpha, cbow_mean, num_threads, train_method, model);
   w2v.gpu_device = gpu;
   w2v.replay_rng = replay != 0;
+  w2v.shared_negatives = shared != 0;
   std::vector<std::vector<std::string>> sentences = read_corpus(input_file.empty() ? "text8" : input_file);
   w2v.build_vocab(sentences);
   w2v.init_weights(w2v.vocab.size());
