@@ -16,7 +16,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 
 
-def counter(path, name, kernel_sub="train_epoch_kernel"):
+def counter(path, name, kernel_sub="train_"):
     vals = []
     for r in csv.DictReader(open(path)):
         if kernel_sub in r["Kernel_Name"] and r["Counter_Name"] == name:
@@ -32,7 +32,7 @@ def main(tag, key):
     fetch = counter(src / "fetch" / "fetch_counter_collection.csv", "FETCH_SIZE")
     write = counter(src / "write" / "write_counter_collection.csv", "WRITE_SIZE")
     stats = list(csv.DictReader(open(src / "kt" / "kt_kernel_stats.csv")))
-    k = [r for r in stats if "train_epoch_kernel" in r["Name"]][0]
+    k = [r for r in stats if "train_" in r["Name"]][0]
     bench = json.loads((src / "kt_bench.json").read_text())
     f_kib = sum(fetch) / len(fetch)
     w_kib = sum(write) / len(write)
