@@ -445,11 +445,14 @@ void cbow_sentence(Orc& m, const int32_t* sent, int len, float alpha, D& dr, int
 
 // Shared-negatives minibatch skip-gram (BASELINE configs[4]; the formulation
 // of Ji et al., "Parallelizing Word2Vec in Shared and Distributed Memory",
-// 2016). NOT a reference function: the reference has no minibatch path. It
-// keeps the reference's subsampling, window shrink, alpha schedule and NS
-// arithmetic (Word2Vec.cpp:251-271, 319-353) but batches one window into a
-// dense update:
-//   inputs  u: the unique context ids of the window (W rows), multiplicity m_u
+// 2016: pWord2Vec). NOT a reference function: the reference has no minibatch
+// path. It keeps the reference's subsampling draw, window shrink, alpha
+// schedule and NS arithmetic (Word2Vec.cpp:251-271, 319-353) but, as
+// word2vec.c and pWord2Vec do, drops subsampled tokens from the sentence
+// before forming windows (the reference keeps them as contexts, :332-347),
+// and batches one window into a dense update:
+//   inputs  u: the unique context ids of the window over the kept tokens (W
+//              rows), multiplicity m_u
 //   outputs t: the center word (label 1, C row) and `negative` draws shared by
 //              the whole window (label 0; a draw equal to the center or to an
 //              earlier draw is dropped — the set semantics of :253-257)
@@ -462,23 +465,30 @@ void cbow_sentence(Orc& m, const int32_t* sent, int len, float alpha, D& dr, int
 template <class D>
 void sgsn_sentence(Orc& m, const int32_t* sent, int len, float alpha, D& dr, int64_t sid) {
   const int d = m.cfg.dim, win = m.cfg.window, K = m.cfg.negative;
-  std::vector<int> in_id, in_m, out_id, out_lab;
-  std::vector<float> E, dW, dC;
-  for (int i = 0; i < len; ++i) {
+  struct Kept { int id, pos, rw; };
+  std::vector<Kept> kept;
+  for (int i = 0; i < len; ++i) {  // the per-token draws, in the reference's order (:331-335)
     const int c = sent[i];
     dr.at(sid, i);
     if (m.keep[c] < dr.uniform()) continue;
-    const int rw = dr.window_shrink();
-    const int lo = std::max(0, i - win + rw), hi = std::min(len, i + win + 1 - rw);
+    kept.push_back({c, i, dr.window_shrink()});
+  }
+  const int nk = (int)kept.size();
+  std::vector<int> in_id, in_m, out_id, out_lab;
+  std::vector<float> E, dW, dC;
+  for (int t = 0; t < nk; ++t) {
+    const int c = kept[t].id, rw = kept[t].rw;
+    const int lo = std::max(0, t - win + rw), hi = std::min(nk, t + win + 1 - rw);
     in_id.clear(); in_m.clear();
     for (int j = lo; j < hi; ++j) {
-      if (j == i) continue;
+      if (j == t) continue;
       size_t u = 0;
-      while (u < in_id.size() && in_id[u] != sent[j]) ++u;
-      if (u == in_id.size()) { in_id.push_back(sent[j]); in_m.push_back(0); }
+      while (u < in_id.size() && in_id[u] != kept[j].id) ++u;
+      if (u == in_id.size()) { in_id.push_back(kept[j].id); in_m.push_back(0); }
       in_m[u] += 1;
     }
     if (in_id.empty()) continue;
+    dr.at(sid, kept[t].pos);
     out_id.assign(1, c);
     out_lab.assign(1, 1);
     for (int k = 0; k < K; ++k) {
@@ -490,28 +500,28 @@ void sgsn_sentence(Orc& m, const int32_t* sent, int len, float alpha, D& dr, int
     const size_t M = in_id.size(), T = out_id.size();
     E.assign(M * T, 0.0f);
     for (size_t u = 0; u < M; ++u)
-      for (size_t t = 0; t < T; ++t) {
-        float f = row_dot(&m.W[(size_t)in_id[u] * d], &m.C[(size_t)out_id[t] * d], d);
+      for (size_t tt = 0; tt < T; ++tt) {
+        float f = row_dot(&m.W[(size_t)in_id[u] * d], &m.C[(size_t)out_id[tt] * d], d);
         f = 1.0 / (1 + std::exp(-f));
-        const float g = (out_lab[t] - f) * alpha;
-        E[u * T + t] = (float)in_m[u] * g;
+        const float g = (out_lab[tt] - f) * alpha;
+        E[u * T + tt] = (float)in_m[u] * g;
       }
     dW.assign(M * d, 0.0f);
     dC.assign(T * d, 0.0f);
     for (size_t u = 0; u < M; ++u)
-      for (size_t t = 0; t < T; ++t) {
-        const float e = E[u * T + t];
+      for (size_t tt = 0; tt < T; ++tt) {
+        const float e = E[u * T + tt];
         const float* wr = &m.W[(size_t)in_id[u] * d];
-        const float* cr = &m.C[(size_t)out_id[t] * d];
+        const float* cr = &m.C[(size_t)out_id[tt] * d];
         for (int k = 0; k < d; ++k) {
           dW[u * d + k] += e * cr[k];
-          dC[t * d + k] += e * wr[k];
+          dC[tt * d + k] += e * wr[k];
         }
       }
     for (size_t u = 0; u < M; ++u)
       for (int k = 0; k < d; ++k) m.W[(size_t)in_id[u] * d + k] += dW[u * d + k];
-    for (size_t t = 0; t < T; ++t)
-      for (int k = 0; k < d; ++k) m.C[(size_t)out_id[t] * d + k] += dC[t * d + k];
+    for (size_t tt = 0; tt < T; ++tt)
+      for (int k = 0; k < d; ++k) m.C[(size_t)out_id[tt] * d + k] += dC[tt * d + k];
   }
 }
 

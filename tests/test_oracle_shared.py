@@ -1,9 +1,10 @@
 """Pin the oracle's shared-negatives minibatch skip-gram (w2v_oracle.cpp:
 sgsn_sentence, BASELINE configs[4]) against an independent numpy restatement
 (float64 GEMMs, Python Philox from tests/refpy.py) on a few sentences. The
-formulation has no reference counterpart, so this restatement plus the
-reference's own pieces it keeps (subsampling draw, window shrink, NS sigmoid
-and label arithmetic, Word2Vec.cpp:251-271, 319-353) is what pins it."""
+formulation has no reference counterpart (it is pWord2Vec's: windows over the
+tokens subsampling keeps), so this restatement plus the reference's own pieces
+it keeps (subsampling draw, window shrink, NS sigmoid and label arithmetic,
+Word2Vec.cpp:251-271, 319-353) is what pins it."""
 import numpy as np
 import pytest
 
@@ -19,21 +20,23 @@ def numpy_sgsn(W, C, keep, table, ids, off, order, window, K, alpha, ts):
     C = C.astype(np.float64)
     for s in order:
         sent = ids[off[s]:off[s + 1]]
-        n = len(sent)
+        kept = []  # (id, position, window shrink) of the tokens subsampling keeps
         for i, c in enumerate(sent):
             t0, t1, _, _ = refpy.philox4x32_10((i, int(s), 0xFFFFFFFF, 0), KEY)
             if keep[c] < refpy.canonical_float(t0):
                 continue
-            rw = (t1 * max(window, 1)) >> 32
-            lo, hi = max(0, i - window + rw), min(n, i + window + 1 - rw)
+            kept.append((int(c), i, (t1 * max(window, 1)) >> 32))
+        n = len(kept)
+        for t, (c, i, rw) in enumerate(kept):
+            lo, hi = max(0, t - window + rw), min(n, t + window + 1 - rw)
             ins, mult = [], []
             for j in range(lo, hi):
-                if j == i:
+                if j == t:
                     continue
-                if sent[j] in ins:
-                    mult[ins.index(sent[j])] += 1
+                if kept[j][0] in ins:
+                    mult[ins.index(kept[j][0])] += 1
                 else:
-                    ins.append(int(sent[j]))
+                    ins.append(kept[j][0])
                     mult.append(1)
             if not ins:
                 continue

@@ -7,11 +7,8 @@
 namespace w2v {
 
 template <int KB, int NW>
-static KernelFn pick_occ(int occ) {
-  switch (occ) {
-    case 3: return &train_shared_neg_kernel<KB, NW, 3>;
-    default: return &train_shared_neg_kernel<KB, NW, 1>;
-  }
+static KernelFn pick_occ(int) {
+  return &train_shared_neg_kernel<KB, NW, 1>;
 }
 
 KernelFn pick_shared_neg(int64_t pitch, int occ, int* waves) {

@@ -35,10 +35,11 @@
 //     the column index on lane & 15, produced per block by a 16x16 transpose
 //     through double-buffered per-wave LDS (row stride 20 floats:
 //     conflict-free reads).
-//   * latency: per 64-token block of the sentence, each wave stages the
-//     block's token ids (with window margins) and the unigram-table draws of
-//     every kept position (dependent random HBM reads) in LDS with one wait;
-//     a center then issues no memory operation before its row gathers.
+//   * windows are word2vec.c's (and pWord2Vec's): subsampled tokens leave the
+//     sentence, so a window spans kept tokens. Each wave compacts the kept
+//     tokens into an LDS ring (ballot + mbcnt) and stages the unigram-table
+//     draws (dependent random HBM reads) of a batch of up to 64 centers with
+//     one wait; a center then issues no memory operation before its gathers.
 //   * Hogwild across workgroups (read-modify-write), the frequent rows with
 //     device-coherent (sc1) loads and write-through stores: see rows_rsrc.
 #pragma once
@@ -50,14 +51,17 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kSnTile = 16;     // MFMA tile edge: context rows, output rows
 constexpr int kSnStride = 20;   // transpose block row stride in floats
+constexpr int kSnRing = 256;    // kept-token ring (holds a 64-center batch, its lookahead and one more block)
 
 template <int NW>
 struct SnShared {
   f32x4 part[2][NW][kWave];                      // partial L tiles, by center parity
   f32x4 e[NW][kWave];                            // per-wave E tile (for its transpose)
   float tr[NW][2][2][kSnTile * kSnStride];       // per-wave transpose blocks [buffer][W, C]
-  int win[NW][2 * kWave];                        // per-wave block ids: positions i0 - 8 .. i0 + 119
-  int draw[NW][kWave][kSnTile];                  // per-wave draws: [position in block][k]
+  int ring_id[NW][kSnRing];                      // per-wave kept tokens of the sentence (ring, by kept index)
+  int ring_pos[NW][kSnRing];                     //   their positions in the sentence
+  int ring_rw[NW][kSnRing];                      //   their window shrinks
+  int draw[NW][kWave][kSnTile];                  // per-wave draws of a batch of <= 64 centers: [center][k]
   uint32_t item[2];                              // dequeued work item, by sentence parity
   float alpha[2];
 };
@@ -140,20 +144,21 @@ __device__ __forceinline__ float sn_grad(float l, bool positive, float alpha) {
   return ((positive ? 1.0f : 0.0f) - f) * alpha;
 }
 
-constexpr int kSnMargin = 8;  // window <= 8: ids of positions [i0 - 8, i0 + 72) cover every window of a block
-
+// Center t (kept index) of the sentence's kept tokens; its window spans kept
+// indices [t - window + rw, t + window + 1 - rw) clipped to [0, nk) (word2vec.c
+// windows: subsampled tokens are gone from the sentence, as in pWord2Vec).
+// Slot b (< 64) of the staged draws belongs to it.
 template <int KB, int NW>
 __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<NW>& sh, __amdgpu_buffer_rsrc_t rW,
-                                          __amdgpu_buffer_rsrc_t rC,
-                                          int wave, int lane, int len, int i0, int b, int c, int rw, float alpha,
-                                          int& par, Counters& cnt, SnProf& pf_) {
+                                          __amdgpu_buffer_rsrc_t rC, int wave, int lane, int t, int nk, int b,
+                                          float alpha, int& par, Counters& cnt, SnProf& pf_) {
   pf_.stamp(0);
   const int q = lane >> 4, col = lane & 15;
-  const int i = i0 + b;
-  const int lo = max(0, i - a.window + rw), hi = min(len, i + a.window + 1 - rw);
+  const int c = sh.ring_id[wave][t & (kSnRing - 1)], rw = sh.ring_rw[wave][t & (kSnRing - 1)];
+  const int lo = max(0, t - a.window + rw), hi = min(nk, t + a.window + 1 - rw);
   const int span = hi - lo;
-  const int wv = sh.win[wave][min(lo - (i0 - kSnMargin) + lane, 2 * kWave - 1)];
-  const int id = (lane < span && lo + lane != i) ? wv : -1;
+  const int wv = sh.ring_id[wave][(lo + lane) & (kSnRing - 1)];
+  const int id = (lane < span && lo + lane != t) ? wv : -1;
   // unique context ids (first occurrence) and their multiplicities
   bool dup = id < 0;
   int mult = 0;
@@ -332,42 +337,56 @@ __global__ __launch_bounds__(NW * kWave, WAVES_PER_SIMD) void train_shared_neg_k
     const int64_t base = a.soff[s];
     const int len = (int)(a.soff[s + 1] - base);
     const int32_t* sent = a.ids + base;
-    for (int i0 = 0; i0 < len; i0 += kWave) {
-      const int ii = i0 + lane;
-      const bool in = ii < len;
-      const int c_l = in ? sent[ii] : 0;
-      const float p_l = in ? a.keep[c_l] : 0.f;
-      uint32_t o0, o1, o2, o3;
-      philox((uint32_t)ii, (uint32_t)s, 0xFFFFFFFFu, a.epoch, a.key0, a.key1, o0, o1, o2, o3);
-      const float u_l = canonical_f(o0);
-      const int rw_l = (int)(((uint64_t)o1 * wmax) >> 32);
-      const bool keep_l = in && !(p_l < u_l);
-      unsigned long long kept = ballot(keep_l);
-      if (!kept) continue;
-      // stage the block's ids (with margins) and every kept position's draws
-      {
-        const int ja = min(max(i0 - kSnMargin + lane, 0), len - 1), jb = min(i0 - kSnMargin + kWave + lane, len - 1);
-        const int va = sent[ja], vb = sent[jb];
+    // Produce kept tokens into the ring 64 positions at a time; consume them
+    // in batches of <= 64 centers once each batch's windows (window kept
+    // tokens past its last center) are in the ring, or the sentence is done.
+    int nk = 0, t_done = 0, i0 = 0;
+    for (;;) {
+      while (i0 < len && nk < t_done + kWave + a.window) {
+        const int ii = i0 + lane;
+        const bool in = ii < len;
+        const int c_l = in ? sent[ii] : 0;
+        const float p_l = in ? a.keep[c_l] : 0.f;
+        uint32_t o0, o1, o2, o3;
+        philox((uint32_t)ii, (uint32_t)s, 0xFFFFFFFFu, a.epoch, a.key0, a.key1, o0, o1, o2, o3);
+        const float u_l = canonical_f(o0);
+        const int rw_l = (int)(((uint64_t)o1 * wmax) >> 32);
+        const bool keep_l = in && !(p_l < u_l);
+        const unsigned long long kept = ballot(keep_l);
+        if (keep_l) {
+          const int r = (nk + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(kept >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((unsigned)kept, 0u))) &
+                        (kSnRing - 1);
+          sh.ring_id[wave][r] = c_l;
+          sh.ring_pos[wave][r] = ii;
+          sh.ring_rw[wave][r] = rw_l;
+        }
+        nk += __popcll(kept);
+        i0 += kWave;
+      }
+      const int n_batch = min(kWave, (i0 >= len ? nk : nk - a.window) - t_done);
+      if (n_batch <= 0) {
+        if (i0 >= len) break;
+        continue;
+      }
+      wave_lds_order();
+      {  // stage the batch's table draws: lane l -> center t_done + l
         int dv[kSnTile];
+        const int pos = sh.ring_pos[wave][(t_done + lane) & (kSnRing - 1)];
 #pragma unroll
         for (int kk = 0; kk < kSnTile; ++kk) {
           dv[kk] = 0;
-          if (keep_l && kk < a.negative)
-            dv[kk] = (int)a.table[philox_table_pos(a, (uint32_t)s, (uint32_t)ii, 0u, (uint32_t)kk)];
+          if (lane < n_batch && kk < a.negative)
+            dv[kk] = (int)a.table[philox_table_pos(a, (uint32_t)s, (uint32_t)pos, 0u, (uint32_t)kk)];
         }
-        sh.win[wave][lane] = va;
-        sh.win[wave][kWave + lane] = vb;
 #pragma unroll
         for (int kk = 0; kk < kSnTile; kk += 4)
           *reinterpret_cast<int4*>(&sh.draw[wave][lane][kk]) = make_int4(dv[kk], dv[kk + 1], dv[kk + 2], dv[kk + 3]);
         wave_lds_order();
       }
-      while (kept) {
-        const int b = __builtin_ctzll(kept);
-        kept &= kept - 1;
-        sn_center<KB, NW>(a, sh, rW, rC, wave, lane, len, i0, b, readlane_i(c_l, b), readlane_i(rw_l, b), alpha, par,
-                          cnt, prof);
-      }
+      for (int b = 0; b < n_batch; ++b)
+        sn_center<KB, NW>(a, sh, rW, rC, wave, lane, t_done + b, nk, b, alpha, par, cnt, prof);
+      t_done += n_batch;
     }
     if (threadIdx.x == 0) atomicAdd(a.words, (unsigned long long)len);
     cnt.sentences += 1;
