@@ -572,15 +572,25 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
       lds_bytes = (size_t)(P * row_bytes) + 16 + (size_t)P * 4;  // + mask, counts, per-row hits
     }
   }
-  if (sn_fn) {  // shared-negatives minibatch: 2-wave workgroups, static LDS, no privatisation
+  if (sn_fn) {  // shared-negatives minibatch: 2-wave workgroups, static LDS
     a.priv_M = nullptr;
-    a.priv_n = 0;
     a.item0 = 0;
+    // LDS-private C rows (kSnPriv in w2v_shared.hpp: 16 KiB of rows, <= 32),
+    // parallel schedule only, written back every flush_centers centers. Off
+    // unless private_rows > 0: measured on configs[4], 8 rows flushed every 64
+    // centers gain 12 % but cost 1.6 points of similarity on the text8-like
+    // gate, and every 16 centers gain nothing (profiles/r01_sn_private_sweep.log).
+    a.priv_n = h->sched == W2V_SCHED_PARALLEL && h->private_rows > 0
+                   ? (int32_t)std::min<int64_t>({(int64_t)32, 16384 / (h->pitch * (int64_t)sizeof(float)), h->V,
+                                                 (int64_t)h->private_rows})
+                   : 0;
+    a.flush_every = h->flush_centers > 0 ? h->flush_centers : 64;
     const int threads = sn_waves * w2v::kWave;
     // device-coherent rows (rows_rsrc in w2v_shared.hpp): all for hot_rows =
     // -1, else at least the rows two XCD L2s' capacity could keep resident
     const int64_t l2_rows = (int64_t)(8 << 20) / (h->pitch * (int64_t)sizeof(float));
     a.hot_wc = h->hot_rows < 0 ? h->V : std::min<int64_t>(h->V, std::max<int64_t>(h->hot_rows, l2_rows));
+    if (const char* e = std::getenv("W2V_SN_COHERENT_ROWS")) a.hot_wc = std::min<int64_t>(h->V, std::atoll(e));  // experiments
     int64_t g = 1;
     if (h->sched == W2V_SCHED_PARALLEL) {
       int per_cu = 0;

@@ -53,15 +53,28 @@ constexpr int kSnTile = 16;     // MFMA tile edge: context rows, output rows
 constexpr int kSnStride = 20;   // transpose block row stride in floats
 constexpr int kSnRing = 256;    // kept-token ring (holds a 64-center batch, its lookahead and one more block)
 
-template <int NW>
+// Private output rows: each workgroup accumulates its updates of the P most
+// frequent C rows (the negatives every center draws) in LDS and writes them
+// back every a.flush_every centers, instead of a coherent read-modify-write
+// of those few rows by every center (their write-through traffic serialises
+// on a handful of memory channels: measured, 16 coherent rows cost a third of
+// the throughput). P fills 16 KiB of LDS, at most 32 rows.
+template <int KB, int NW>
+constexpr int kSnPriv = (16384 / (NW * KB * 64)) < 32 ? (16384 / (NW * KB * 64)) : 32;
+
+template <int KB, int NW>
 struct SnShared {
   f32x4 part[2][NW][kWave];                      // partial L tiles, by center parity
   f32x4 e[NW][kWave];                            // per-wave E tile (for its transpose)
   float tr[NW][2][2][kSnTile * kSnStride];       // per-wave transpose blocks [buffer][W, C]
-  int ring_id[NW][kSnRing];                      // per-wave kept tokens of the sentence (ring, by kept index)
-  int ring_pos[NW][kSnRing];                     //   their positions in the sentence
-  int ring_rw[NW][kSnRing];                      //   their window shrinks
-  int draw[NW][kWave][kSnTile];                  // per-wave draws of a batch of <= 64 centers: [center][k]
+  // written identically by every wave (read only before the per-center
+  // barrier, rewritten only after it): the kept tokens of the sentence (ring,
+  // by kept index) and the draws of a batch of <= 64 centers
+  int ring_id[kSnRing];
+  int ring_pos[kSnRing];                         //   positions in the sentence
+  int ring_rw[kSnRing];                          //   window shrinks
+  int draw[kWave][kSnTile];                      // [center in batch][k]
+  float priv[kSnPriv<KB, NW>][NW * KB * kSnTile];  // pending deltas of C rows [0, P); wave w owns its columns
   uint32_t item[2];                              // dequeued work item, by sentence parity
   float alpha[2];
 };
@@ -149,15 +162,15 @@ __device__ __forceinline__ float sn_grad(float l, bool positive, float alpha) {
 // windows: subsampled tokens are gone from the sentence, as in pWord2Vec).
 // Slot b (< 64) of the staged draws belongs to it.
 template <int KB, int NW>
-__device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<NW>& sh, __amdgpu_buffer_rsrc_t rW,
+__device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<KB, NW>& sh, __amdgpu_buffer_rsrc_t rW,
                                           __amdgpu_buffer_rsrc_t rC, int wave, int lane, int t, int nk, int b,
                                           float alpha, int& par, Counters& cnt, SnProf& pf_) {
   pf_.stamp(0);
   const int q = lane >> 4, col = lane & 15;
-  const int c = sh.ring_id[wave][t & (kSnRing - 1)], rw = sh.ring_rw[wave][t & (kSnRing - 1)];
+  const int c = sh.ring_id[t & (kSnRing - 1)], rw = sh.ring_rw[t & (kSnRing - 1)];
   const int lo = max(0, t - a.window + rw), hi = min(nk, t + a.window + 1 - rw);
   const int span = hi - lo;
-  const int wv = sh.ring_id[wave][(lo + lane) & (kSnRing - 1)];
+  const int wv = sh.ring_id[(lo + lane) & (kSnRing - 1)];
   const int id = (lane < span && lo + lane != t) ? wv : -1;
   // unique context ids (first occurrence) and their multiplicities
   bool dup = id < 0;
@@ -194,7 +207,7 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<NW>& sh, 
   for (int kb = 0; kb < KB; ++kb) wr[kb] = load_row4(rW, wo + 64u * kb, w_coh);
   // outputs: lane 0 the center, lane t in [1, K] the (t-1)-th shared draw
   const int K = a.negative;
-  const int prev_draw = sh.draw[wave][b][(lane + kSnTile - 1) & (kSnTile - 1)];
+  const int prev_draw = sh.draw[b][(lane + kSnTile - 1) & (kSnTile - 1)];
   const int out_l = (lane == 0) ? c : prev_draw;
   bool ok = (lane == 0) || (lane <= K && out_l != c);
   for (int j = 1; j < K; ++j) {
@@ -206,6 +219,8 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<NW>& sh, 
   const int out_row = __shfl(out_l, out_ok ? col : 0);
   const uint32_t co = (uint32_t)(((int64_t)out_row * a.pitch + cb) * 4);
   const bool c_coh = out_row < a.hot_wc;
+  const bool c_priv = out_row < a.priv_n;  // this workgroup's pending delta lives in LDS
+  float* pr = &sh.priv[c_priv ? out_row : 0][(int)cb];
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) cr[kb] = load_row4(rC, co + 64u * kb, c_coh);
   cnt.centers += 1;
@@ -214,6 +229,10 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<NW>& sh, 
   cnt.draws += (unsigned long long)K;
   pf_.stamp(1);
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  if (c_priv) {
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) cr[kb] += *reinterpret_cast<const f32x4*>(pr + kSnTile * kb);
+  }
   // unused slots hold slot 0's row: finite, and every E term that touches them
   // is masked to zero below, so they add nothing to dW, dC (and are not stored)
   pf_.stamp(2);
@@ -286,19 +305,42 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<NW>& sh, 
     }
     wr[kb] += dw;
     cr[kb] += dc;
+    if (c_priv && out_ok) *reinterpret_cast<f32x4*>(pr + kSnTile * kb) += dc;
     if (kb & 1) {  // blocks kb - 1, kb written back as whole 128-B lines
       store_pair(wr[kb - 1], wr[kb], rW, wo + 64u * (kb - 1), in_ok, w_coh, col);
-      store_pair(cr[kb - 1], cr[kb], rC, co + 64u * (kb - 1), out_ok, c_coh, col);
+      store_pair(cr[kb - 1], cr[kb], rC, co + 64u * (kb - 1), out_ok && !c_priv, c_coh, col);
     }
   }
   pf_.stamp(6);
+}
+
+// Write this wave's columns of the private rows' pending deltas back to C
+// (coherent read-modify-write, as every other frequent row) and clear them.
+template <int KB, int NW>
+__device__ __forceinline__ void sn_flush_private(const TrainArgs& a, SnShared<KB, NW>& sh, __amdgpu_buffer_rsrc_t rC,
+                                                 int wave, int lane) {
+  constexpr int kCols = KB * kSnTile;  // this wave's columns of a row
+  for (int r = 0; r < a.priv_n; ++r) {
+#pragma unroll
+    for (int c0 = 0; c0 < kCols; c0 += 4 * kWave) {
+      const int cc = c0 + 4 * lane;
+      if (cc < kCols) {
+        float* p = &sh.priv[r][wave * kCols + cc];
+        const f32x4 dlt = *reinterpret_cast<f32x4*>(p);
+        const uint32_t off = (uint32_t)(((int64_t)r * a.pitch + wave * kCols + cc) * 4);
+        const f32x4 v = load_row4(rC, off, true) + dlt;
+        store_row4(v, rC, off, true);
+        *reinterpret_cast<f32x4*>(p) = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
 }
 
 // Epoch kernel: workgroups dequeue sentences (Word2Vec.cpp:375-394) and walk
 // them with the reference's subsampling and window shrink (Philox draws).
 template <int KB, int NW, int WAVES_PER_SIMD>
 __global__ __launch_bounds__(NW * kWave, WAVES_PER_SIMD) void train_shared_neg_kernel(TrainArgs a) {
-  __shared__ SnShared<NW> sh;
+  __shared__ SnShared<KB, NW> sh;
   const int lane = lane_id();
   const int wave = (int)(threadIdx.x >> 6);
   Counters cnt;
@@ -308,6 +350,11 @@ __global__ __launch_bounds__(NW * kWave, WAVES_PER_SIMD) void train_shared_neg_k
 #endif
   const __amdgpu_buffer_rsrc_t rW = rows_rsrc(a.W), rC = rows_rsrc(a.C);
   int par = 0;
+  int since_flush = 0;  // centers since the private rows were written back
+  if (a.priv_n > 0) {
+    for (int k = threadIdx.x; k < kSnPriv<KB, NW> * NW * KB * kSnTile; k += blockDim.x) (&sh.priv[0][0])[k] = 0.f;
+    __syncthreads();
+  }
   float alpha0 = a.init_alpha;  // thread 0's schedule state
   bool first = true;
   const uint32_t wmax = (uint32_t)(a.window < 1 ? 1 : a.window);
@@ -357,9 +404,9 @@ __global__ __launch_bounds__(NW * kWave, WAVES_PER_SIMD) void train_shared_neg_k
           const int r = (nk + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(kept >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((unsigned)kept, 0u))) &
                         (kSnRing - 1);
-          sh.ring_id[wave][r] = c_l;
-          sh.ring_pos[wave][r] = ii;
-          sh.ring_rw[wave][r] = rw_l;
+          sh.ring_id[r] = c_l;
+          sh.ring_pos[r] = ii;
+          sh.ring_rw[r] = rw_l;
         }
         nk += __popcll(kept);
         i0 += kWave;
@@ -372,7 +419,7 @@ __global__ __launch_bounds__(NW * kWave, WAVES_PER_SIMD) void train_shared_neg_k
       wave_lds_order();
       {  // stage the batch's table draws: lane l -> center t_done + l
         int dv[kSnTile];
-        const int pos = sh.ring_pos[wave][(t_done + lane) & (kSnRing - 1)];
+        const int pos = sh.ring_pos[(t_done + lane) & (kSnRing - 1)];
 #pragma unroll
         for (int kk = 0; kk < kSnTile; ++kk) {
           dv[kk] = 0;
@@ -381,16 +428,22 @@ __global__ __launch_bounds__(NW * kWave, WAVES_PER_SIMD) void train_shared_neg_k
         }
 #pragma unroll
         for (int kk = 0; kk < kSnTile; kk += 4)
-          *reinterpret_cast<int4*>(&sh.draw[wave][lane][kk]) = make_int4(dv[kk], dv[kk + 1], dv[kk + 2], dv[kk + 3]);
+          *reinterpret_cast<int4*>(&sh.draw[lane][kk]) = make_int4(dv[kk], dv[kk + 1], dv[kk + 2], dv[kk + 3]);
         wave_lds_order();
       }
-      for (int b = 0; b < n_batch; ++b)
+      for (int b = 0; b < n_batch; ++b) {
         sn_center<KB, NW>(a, sh, rW, rC, wave, lane, t_done + b, nk, b, alpha, par, cnt, prof);
+        if (a.priv_n > 0 && ++since_flush >= a.flush_every) {
+          sn_flush_private<KB, NW>(a, sh, rC, wave, lane);
+          since_flush = 0;
+        }
+      }
       t_done += n_batch;
     }
     if (threadIdx.x == 0) atomicAdd(a.words, (unsigned long long)len);
     cnt.sentences += 1;
   }
+  if (a.priv_n > 0) sn_flush_private<KB, NW>(a, sh, rC, wave, lane);
 #ifdef W2V_SN_PROF
   prof.stamp(0);
   if (lane == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))
