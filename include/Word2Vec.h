@@ -114,6 +114,16 @@ class Word2Vec {
   // Word2Vec.cpp:362-363 (raw tokens incl. OOV). For corpora too large for
   // vector<vector<string>>.
   void train_ids(const std::vector<int32_t>& ids, const std::vector<int64_t>& offsets, int64_t train_words);
+  // Corpus files too large for vector<vector<string>> (mapped, tokenised by
+  // host threads; threads <= 0 = all): format "lines" reads like line_docs
+  // (Word2Vec.cpp:19-30), "text8" like the reference CLI (main.cpp:63-92,
+  // 1000-token sentences). Same vocabulary (bit-exact), samples and
+  // train_words as build_vocab / train on the sentences those readers return.
+  void build_vocab_file(const std::string& path, const std::string& format = "lines", int threads = 0);
+  void train_file(const std::string& path, const std::string& format = "lines", int threads = 0);
+  // build_sample of a corpus file as token ids (what train_file trains on).
+  void file_samples(const std::string& path, const std::string& format, int threads, std::vector<int32_t>& ids,
+                    std::vector<int64_t>& offsets, int64_t& train_words);
   // Last device error (empty if none).
   std::string last_error;
 
@@ -124,6 +134,7 @@ class Word2Vec {
   int64_t cur_words_ = 0;           // current_words after the last train call
 
   bool uses_C() const;
+  void finish_vocab(std::unordered_map<std::string, int>& tally);
   void ensure_device();
   void upload_vocab_products();
   void check(int rc, const char* what);

@@ -37,6 +37,16 @@ int w2v_model_train(w2v_model* m, const char* text, int64_t len);
 int w2v_model_train_ids(w2v_model* m, const int32_t* ids, const int64_t* offsets, int64_t n_sent,
                         int64_t train_words);
 int w2v_model_init_weights(w2v_model* m);
+/* Corpus files (Word2Vec::build_vocab_file / train_file / file_samples):
+ * format "lines" (line_docs) or "text8" (the reference CLI's reader); threads
+ * <= 0 = all host threads. w2v_model_file_samples tokenises the file and keeps
+ * the result in the handle; w2v_model_copy_samples copies it out (ids:
+ * *n_tokens int32, offsets: *n_sentences + 1 int64). */
+int w2v_model_build_vocab_file(w2v_model* m, const char* path, const char* format, int32_t threads);
+int w2v_model_train_file(w2v_model* m, const char* path, const char* format, int32_t threads);
+int w2v_model_file_samples(w2v_model* m, const char* path, const char* format, int32_t threads, int64_t* n_tokens,
+                           int64_t* n_sentences, int64_t* train_words);
+int w2v_model_copy_samples(w2v_model* m, int32_t* ids, int64_t* offsets);
 
 int64_t w2v_model_vocab_size(w2v_model* m);
 const char* w2v_model_word(w2v_model* m, int64_t i);

@@ -16,6 +16,7 @@
 #include <sstream>
 #include <stdexcept>
 
+#include "w2v_corpus.h"
 #include "w2v_dev.h"
 #include "w2v_host.h"
 
@@ -109,6 +110,43 @@ void Word2Vec::build_vocab(std::vector<std::vector<std::string>>& sentences) {
       if (tally.count(w) > 0) tally[w]++;
       else tally[w] = 1;
     }
+  finish_vocab(tally);
+}
+
+// The counting map's iteration order depends only on the order in which the
+// distinct words were first inserted, so a file's counts inserted in order of
+// first occurrence give the map build_vocab builds (corpus.cpp).
+void Word2Vec::build_vocab_file(const std::string& path, const std::string& format, int threads) {
+  const w2v_corpus::File f(path);
+  const w2v_corpus::Counts c = w2v_corpus::count_words(f, w2v_corpus::parse_format(format), threads);
+  std::unordered_map<std::string, int> tally;
+  for (const auto& wc : c.words) tally[wc.first] = (int)wc.second;
+  finish_vocab(tally);
+}
+
+void Word2Vec::file_samples(const std::string& path, const std::string& format, int threads,
+                            std::vector<int32_t>& ids, std::vector<int64_t>& offsets, int64_t& train_words) {
+  std::unordered_map<std::string, int32_t> index;
+  index.reserve(vocab.size());
+  for (const Word* w : vocab) index[w->text] = (int32_t)w->index;
+  const w2v_corpus::File f(path);
+  w2v_corpus::Samples s = w2v_corpus::samples(f, w2v_corpus::parse_format(format), threads, index);
+  ids.swap(s.ids);
+  offsets.swap(s.offsets);
+  train_words = s.raw_tokens;
+}
+
+void Word2Vec::train_file(const std::string& path, const std::string& format, int threads) {
+  std::vector<int32_t> ids;
+  std::vector<int64_t> offsets;
+  int64_t train_words = 0;
+  file_samples(path, format, threads, ids, offsets, train_words);
+  train_ids(ids, offsets, train_words);
+}
+
+// Word2Vec.cpp:143-168: keep >= min_count in the map's iteration order,
+// std::sort by count desc, index, then the vocab products.
+void Word2Vec::finish_vocab(std::unordered_map<std::string, int>& tally) {
   for (auto kv : tally) {
     if (kv.second < min_count) continue;
     Word* w = new Word(0, (size_t)kv.second, kv.first);

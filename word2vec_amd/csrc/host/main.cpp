@@ -55,24 +55,6 @@ int find_flag(const char* name, int argc, char** argv) {
   return -1;
 }
 
-// main.cpp:63-92: whitespace tokens grouped into 1000-token sentences.
-std::vector<std::vector<std::string>> read_corpus(const std::string& path) {
-  const size_t kSentence = 1000;
-  std::vector<std::vector<std::string>> out;
-  std::ifstream in(path);
-  std::vector<std::string> cur;
-  std::string tok;
-  while (in >> tok) {
-    cur.push_back(tok);
-    if (cur.size() == kSentence) {
-      out.push_back(cur);
-      cur.clear();
-    }
-  }
-  if (!cur.empty()) out.push_back(cur);
-  return out;
-}
-
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -134,12 +116,20 @@ int main(int argc, char** argv) {
   w2v.gpu_device = gpu;
   w2v.replay_rng = replay != 0;
   w2v.shared_negatives = shared != 0;
-  std::vector<std::vector<std::string>> sentences = read_corpus(input_file.empty() ? "text8" : input_file);
-  w2v.build_vocab(sentences);
+  // main.cpp:63-92's reader (1000-token sentences), streamed from the mapped
+  // file by host threads: the same vocabulary and samples as building
+  // vector<vector<string>> first (Word2Vec::build_vocab_file / train_file)
+  const std::string corpus = input_file.empty() ? "text8" : input_file;
+  try {
+    w2v.build_vocab_file(corpus, "text8");
+  } catch (const std::exception& e) {
+    std::cerr << e.what() << std::endl;
+    return 1;
+  }
   w2v.init_weights(w2v.vocab.size());
   if (!save_vocab_file.empty()) w2v.save_vocab(save_vocab_file);
   try {
-    w2v.train(sentences);
+    w2v.train_file(corpus, "text8");
   } catch (const std::exception& e) {
     std::cerr << e.what() << std::endl;
     return 2;

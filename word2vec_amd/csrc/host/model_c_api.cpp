@@ -10,6 +10,8 @@
 struct w2v_model {
   Word2Vec w;
   std::string err;
+  std::vector<int32_t> ids;       // w2v_model_file_samples
+  std::vector<int64_t> offsets;
   w2v_model(int iter, int window, int min_count, int table_size, int dim, int negative, float sub, float a0,
             float a1, bool mean, int threads, const char* tm, const char* mdl)
       : w(iter, window, min_count, table_size, dim, negative, sub, a0, a1, mean, threads, tm, mdl) {}
@@ -101,6 +103,32 @@ int w2v_model_train_ids(w2v_model* m, const int32_t* ids, const int64_t* off, in
     m->w.train_ids(i, o, tw);
   });
 }
+int w2v_model_build_vocab_file(w2v_model* m, const char* path, const char* format, int32_t threads) {
+  return guard(m, [&] { m->w.build_vocab_file(path, format, threads); });
+}
+
+int w2v_model_train_file(w2v_model* m, const char* path, const char* format, int32_t threads) {
+  return guard(m, [&] { m->w.train_file(path, format, threads); });
+}
+
+int w2v_model_file_samples(w2v_model* m, const char* path, const char* format, int32_t threads, int64_t* n_tokens,
+                           int64_t* n_sentences, int64_t* train_words) {
+  return guard(m, [&] {
+    int64_t tw = 0;
+    m->w.file_samples(path, format, threads, m->ids, m->offsets, tw);
+    if (n_tokens) *n_tokens = (int64_t)m->ids.size();
+    if (n_sentences) *n_sentences = (int64_t)m->offsets.size() - 1;
+    if (train_words) *train_words = tw;
+  });
+}
+
+int w2v_model_copy_samples(w2v_model* m, int32_t* ids, int64_t* offsets) {
+  return guard(m, [&] {
+    if (ids && !m->ids.empty()) std::memcpy(ids, m->ids.data(), m->ids.size() * sizeof(int32_t));
+    if (offsets) std::memcpy(offsets, m->offsets.data(), m->offsets.size() * sizeof(int64_t));
+  });
+}
+
 int w2v_model_init_weights(w2v_model* m) {
   return guard(m, [&] { m->w.init_weights(m->w.vocab.size()); });
 }

@@ -35,6 +35,10 @@ def _load():
             "w2v_model_train": (C.c_int, [P, S, I64]),
             "w2v_model_train_ids": (C.c_int, [P, P, P, I64, I64]),
             "w2v_model_init_weights": (C.c_int, [P]),
+            "w2v_model_build_vocab_file": (C.c_int, [P, S, S, I32]),
+            "w2v_model_train_file": (C.c_int, [P, S, S, I32]),
+            "w2v_model_file_samples": (C.c_int, [P, S, S, I32, C.POINTER(I64), C.POINTER(I64), C.POINTER(I64)]),
+            "w2v_model_copy_samples": (C.c_int, [P, P, P]),
             "w2v_model_vocab_size": (I64, [P]),
             "w2v_model_word": (S, [P, I64]),
             "w2v_model_word_count": (I64, [P, I64]),
@@ -115,6 +119,26 @@ class Word2Vec:
     def train(self, sentences):
         t = _text(sentences)
         self._chk(self.L.w2v_model_train(self.h, t, len(t)), "train")
+
+    def build_vocab_file(self, path, format="lines", threads=0):
+        """Word2Vec::build_vocab_file: the vocab of a corpus file, bit-exact with build_vocab(line_docs(path))
+        ("lines") or with the reference CLI's text8 reader ("text8")."""
+        self._chk(self.L.w2v_model_build_vocab_file(self.h, str(path).encode(), format.encode(), int(threads)),
+                  "build_vocab_file")
+
+    def train_file(self, path, format="lines", threads=0):
+        self._chk(self.L.w2v_model_train_file(self.h, str(path).encode(), format.encode(), int(threads)),
+                  "train_file")
+
+    def file_samples(self, path, format="lines", threads=0):
+        """(ids, offsets, train_words): build_sample of a corpus file as token ids."""
+        nt, ns, tw = C.c_int64(), C.c_int64(), C.c_int64()
+        self._chk(self.L.w2v_model_file_samples(self.h, str(path).encode(), format.encode(), int(threads),
+                                                C.byref(nt), C.byref(ns), C.byref(tw)), "file_samples")
+        ids = np.empty(nt.value, np.int32)
+        off = np.empty(ns.value + 1, np.int64)
+        self._chk(self.L.w2v_model_copy_samples(self.h, _p(ids), _p(off)), "copy_samples")
+        return ids, off, tw.value
 
     def train_ids(self, ids, offsets, train_words):
         ids = np.ascontiguousarray(ids, np.int32)
