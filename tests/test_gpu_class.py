@@ -113,3 +113,26 @@ def test_cli_end_to_end(tmp_path):
     assert d == 64 and len(lines) == V + 1 == len(vocab.read_text().splitlines()) + 1
     vals = np.array([float(x) for x in lines[1].split()[1:]])
     assert vals.size == 64 and np.isfinite(vals).all()
+
+
+@pytest.mark.parametrize("mode", ["sg_ns", "cbow_hs"])
+def test_class_train_file_equals_train(tmp_path, mode):
+    """train_file (mapped corpus, threaded tokenisation) trains exactly what
+    train(line_docs(path)) does: replay mode is deterministic, so the matrices
+    must be identical."""
+    sents = zipf_sentences(20, 150, 300, seed=17, ragged=True)
+    path = tmp_path / "c.txt"
+    path.write_text("\n".join(" ".join(s) for s in sents) + "\n")
+    a = _pair(mode, sents, iters=1)
+    a.train(sents)
+    m = MODES[mode]
+    b = Word2Vec(iter=1, window=5, min_count=2, table_size=50_000, word_dim=32, negative=m["negative"],
+                 subsample_threshold=1e-3, init_alpha=0.05, min_alpha=2.5e-6, cbow_mean=True,
+                 train_method=m["train_method"], model=m["model"], replay_rng=True)
+    b.seed(5)
+    b.build_vocab_file(path, "lines", 2)
+    b.init_weights()
+    b.train_file(path, "lines", 2)
+    assert a.vocab()[0] == b.vocab()[0]
+    for k in range(3):
+        np.testing.assert_array_equal(a.matrix(k), b.matrix(k))
