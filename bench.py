@@ -38,12 +38,24 @@ MODES = {
 }
 MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X dense f32-input MFMA (MI355X_MICROARCH.md)
 
+# BASELINE.json configs on this bench's synthetic Zipf corpora (text8 and the
+# 1B-Word corpus are not available offline): --config cN sets these fields.
+CONFIGS = {
+    "c1": dict(mode="sg_ns", dim=100, negative=5, vocab=250_000, tokens=17_000_000),    # text8-shaped SGNS d100
+    "c2": dict(mode="cbow_hs", dim=200, negative=0, vocab=250_000, tokens=17_000_000),  # text8-shaped CBOW-HS d200
+    "c3": dict(mode="sg_ns", dim=300, negative=5, vocab=1_000_000, tokens=50_000_000),  # 1B-Word stand-in (default)
+    "c4": dict(mode="sg_ns", dim=300, negative=5, vocab=1_000_000, tokens=50_000_000),  # per GPU of the N-GPU run
+    "c5": dict(mode="sg_sn", dim=512, negative=15, vocab=1_000_000, tokens=50_000_000),  # shared-negatives MFMA
+}
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", choices=list(CONFIGS), default=None,
+                    help="BASELINE.json config preset (overrides --mode/--dim/--negative/--vocab/--tokens)")
     ap.add_argument("--mode", default="sg_ns", choices=list(MODES))
     ap.add_argument("--dim", type=int, default=300)
     ap.add_argument("--negative", type=int, default=5)
@@ -71,7 +83,11 @@ def parse():
                     help="N=1 only: let the library allocate the matrices instead of torch")
     ap.add_argument("--sync-every", type=int, default=0,
                     help="average the replicas every this many sentences of a shard (0 = once per step)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.config:
+        for k, v in CONFIGS[args.config].items():
+            setattr(args, k, v)
+    return args
 
 
 def log(*a):
@@ -270,7 +286,8 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": (f"trained words/sec, dim={d} SGNS" + (" shared-negatives minibatch" if mode.get("shared") else "")
+            "metric": (f"trained words/sec, dim={d} " + ("CBOW" if mode["cbow"] else "SG") + ("-HS" if mode["hs"] else ("-NS" if mode["cbow"] else "NS"))
+                       + (" shared-negatives minibatch" if mode.get("shared") else "")
                        + " (per-GPU replica, RCCL model averaging for N>1)"),
             "value": round(value, 1),
             "unit": "words/s",
@@ -286,8 +303,13 @@ def main():
             "config": {
                 "workload": f"{args.mode} neg{neg} d{d} w{args.window} subsample {args.subsample} min_count "
                             f"{args.min_count}; synthetic Zipf(s={args.zipf_s:g}) over {args.vocab} ranks "
-                            + ("(configs[4], shared-negatives minibatch)" if mode.get("shared") else
-                               "standing in for 1B-Word (configs[2])") + f"; {args.sent_len}-token sentences",
+                            + {"c1": "standing in for text8 (configs[0]'s workload)",
+                               "c2": "standing in for text8 (configs[1])",
+                               "c4": "per GPU of configs[3]",
+                               "c5": "(configs[4], shared-negatives minibatch)"}.get(
+                                   args.config, "(configs[4], shared-negatives minibatch)" if mode.get("shared") else
+                                   "standing in for 1B-Word (configs[2])") + f"; {args.sent_len}-token sentences",
+                "baseline_config": args.config or ("c5" if mode.get("shared") else "c3"),
                 "tokens_per_gpu_per_step": n_tok,
                 "in_vocab_tokens_per_gpu_per_step": int(ids_h.size),
                 "vocab_size": V,
