@@ -78,6 +78,9 @@ def parse():
                     help="workgroup centers between private-row flushes (0 = auto)")
     ap.add_argument("--private-average", type=float, default=8.0,
                     help="concurrency the private rows' summed deltas are scaled to (0 = plain sum)")
+    ap.add_argument("--context-rows", type=int, default=-1,
+                    help="CBOW: hottest context rows privatised in LDS (-1 auto, 0 off)")
+    ap.add_argument("--context-flush", type=int, default=0, help="CBOW: centers between context-row flushes (0 auto)")
     ap.add_argument("--max-waves", type=int, default=0, help="wavefronts in flight (0 = all that fit)")
     ap.add_argument("--own-model", action="store_true",
                     help="N=1 only: let the library allocate the matrices instead of torch")
@@ -208,6 +211,7 @@ def main():
     tr.set_private_rows(args.private_rows)
     tr.set_private_sync(args.flush_centers, args.private_average)
     tr.set_max_waves(args.max_waves)
+    tr.set_context_private(args.context_rows, args.context_flush)
     tr.set_progress(0)
     torch.cuda.synchronize()
     log(f"[bench] resident in HBM ({time.time() - t0:.1f}s)")
@@ -321,6 +325,8 @@ def main():
                 "flush_centers": args.flush_centers,
                 "private_average": args.private_average,
                 "max_waves": args.max_waves,
+                "context_rows": args.context_rows,
+                "context_flush": args.context_flush,
                 "kept_centers_per_step": int(delta["centers"] / args.steps),
                 "targets_per_step": int(delta["targets"] / args.steps),
             },

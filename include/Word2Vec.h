@@ -103,6 +103,8 @@ class Word2Vec {
   int flush_centers = 0;        // workgroup centers between private-row flushes (0 = auto)
   float private_average = 8.f;  // concurrency the private rows' summed deltas are scaled to (0 = sum)
   int64_t max_waves = 0;        // wavefronts in flight (0 = as many as fit)
+  int context_rows = -1;        // CBOW: hottest context rows privatised in LDS too: -1 as many as fit, 0 off
+  int context_flush = 0;        // workgroup centers between context-row flushes (0 = auto)
   // BASELINE configs[4]: skip-gram NS as the shared-negatives minibatch on the
   // matrix cores (w2v_dev_set_update, W2V_UPDATE_SHARED_NEGATIVES) instead of
   // the reference's per-pair update; sg + ns only, negative <= 15, window <= 8

@@ -179,6 +179,14 @@ int w2v_dev_set_private_rows(w2v_dev* h, int32_t n);
  * for HS); average_over: the concurrency a private row's summed deltas are
  * scaled down to (default 8; 0 = plain sum). */
 int w2v_dev_set_private_sync(w2v_dev* h, int32_t flush_centers, float average_over);
+/* CBOW only: privatise the `rows` hottest context rows of C (a window's
+ * contexts are not subsampled, Word2Vec.cpp:286-300, so the most frequent
+ * words sit in most windows) in LDS as well, beside the output rows, flushed
+ * every flush_centers workgroup centers with the same averaging. rows: -1 =
+ * auto (CBOW-HS: as many as fit beside the output rows, at most 64; CBOW-NS:
+ * none); 0 = off (those rows then take the hot-row
+ * atomics). flush_centers: 0 = auto (32 for HS, 256 for NS). */
+int w2v_dev_set_context_private(w2v_dev* h, int32_t rows, int32_t flush_centers);
 /* Cap on wavefronts in flight in the parallel schedule (0 = as many as fit,
  * the default). Fewer wavefronts, less staleness, less throughput. */
 int w2v_dev_set_max_waves(w2v_dev* h, int64_t n);

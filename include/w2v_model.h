@@ -28,6 +28,8 @@ void w2v_model_options(w2v_model* m, int32_t gpu_device, int32_t replay_rng, int
 /* Parallel-schedule update policy (Word2Vec.h additive members; include/w2v_dev.h). */
 void w2v_model_update_policy(w2v_model* m, int64_t hot_rows, int32_t private_rows, int32_t flush_centers,
                              float private_average, int64_t max_waves);
+/* CBOW context-row privatisation (Word2Vec.h context_rows / context_flush; w2v_dev_set_context_private). */
+void w2v_model_context_policy(w2v_model* m, int32_t context_rows, int32_t context_flush);
 /* Word2Vec::shared_negatives (configs[4] minibatch skip-gram; include/w2v_dev.h w2v_dev_set_update). */
 void w2v_model_set_shared_negatives(w2v_model* m, int32_t on);
 

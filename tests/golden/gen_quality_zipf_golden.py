@@ -1,6 +1,9 @@
 """Oracle scores on the text8-like planted corpus (tests/quality.planted_zipf_corpus),
-SG-NS, 3 seeds -> tests/golden/quality_zipf_oracle.json (about 2 min per seed,
-the seeds run in parallel processes). Run from the repo root."""
+3 seeds: SG-NS -> tests/golden/quality_zipf_oracle.json, CBOW-HS (configs[1]'s
+mode; `python tests/golden/gen_quality_zipf_golden.py cbow_hs`) ->
+tests/golden/quality_zipf_cbow_hs_oracle.json, the shared-negatives
+minibatch (`... sg_sn`) -> tests/golden/quality_zipf_sg_sn_oracle.json. About 2 min per seed, the seeds
+run in parallel processes. Run from the repo root."""
 import json
 import sys
 from concurrent.futures import ProcessPoolExecutor
@@ -13,28 +16,47 @@ ZCORPUS = dict(n_tokens=10_000_000, sent_len=1000, planted_frac=0.10, seed=0)
 ZTRAIN = dict(dim=100, window=5, iters=1, table_size=100_000_000, min_count=5, subsample=1e-4)
 ZMODE = "sg_ns"
 ZSEEDS = (1, 2, 3)
+ZFILES = {"sg_ns": "quality_zipf_oracle.json", "cbow_hs": "quality_zipf_cbow_hs_oracle.json",
+          "sg_sn": "quality_zipf_sg_sn_oracle.json"}
 
 
-def one(seed):
+def zalpha(mode):
+    return 0.025 if mode.startswith("sg") else 0.05
+
+
+def zmatrix(mode):
+    """The vectors evaluated: W, or C for CBOW-HS (tests/test_gpu_quality.train_gpu)."""
+    return 1 if mode == "cbow_hs" else 0
+
+
+def one(seed, mode=ZMODE):
     from tests.harness import oracle_run
     from tests.quality import planted_zipf_corpus
     from word2vec_amd.evaluate import analogy_accuracy, similarity_score
 
     sents, qs, pairs = planted_zipf_corpus(**ZCORPUS)
-    o = oracle_run(sents, ZMODE, seed=seed, init_alpha=0.025, **ZTRAIN)
+    if mode == "sg_sn":  # configs[4]'s shared-negatives minibatch, sequential (oracle sgsn_sentence), neg 5
+        import numpy as np
+        o = oracle_run(sents, "sg_ns", seed=seed, init_alpha=zalpha(mode), train=False, **ZTRAIN)
+        o.build_sample()
+        o.set_shared_negatives(True)
+        order = np.random.default_rng(seed).permutation(len(sents)).astype(np.int64)
+        o.train_philox(0, 1, order, 0x5EED0000 + seed, 0)
+    else:
+        o = oracle_run(sents, mode, seed=seed, init_alpha=zalpha(mode), **ZTRAIN)
     words, _ = o.vocab()
-    E = o.matrix(0)
+    E = o.matrix(zmatrix(mode))
     return {"seed": seed, "analogy": analogy_accuracy(words, E, qs)["accuracy"],
             "similarity": similarity_score(words, E, pairs)["spearman"], "V": len(words)}
 
 
-def main():
+def main(mode=ZMODE):
     with ProcessPoolExecutor(len(ZSEEDS)) as ex:
-        res = list(ex.map(one, ZSEEDS))
-    out = {"corpus": ZCORPUS, "train": ZTRAIN, "mode": ZMODE, "scores": res}
-    (ROOT / "tests" / "golden" / "quality_zipf_oracle.json").write_text(json.dumps(out, indent=1) + "\n")
+        res = list(ex.map(one, ZSEEDS, [mode] * len(ZSEEDS)))
+    out = {"corpus": ZCORPUS, "train": ZTRAIN, "mode": mode, "alpha": zalpha(mode), "scores": res}
+    (ROOT / "tests" / "golden" / ZFILES[mode]).write_text(json.dumps(out, indent=1) + "\n")
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
-    main()
+    main(*sys.argv[1:2])

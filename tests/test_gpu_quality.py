@@ -4,8 +4,8 @@ default update policy): analogy (3CosAdd accuracy) and word similarity
 (Spearman x100) must not fall more than 1 point below the oracle's
 (sequential reference restatement), on
   * the planted-relation corpus (4 modes, 3 seeds each side) and
-  * the text8-like planted Zipf corpus (SG-NS, V~98K, 10K 1000-token
-    sentences; oracle golden over 3 seeds).
+  * the text8-like planted Zipf corpus (SG-NS and CBOW-HS, V~98K, 10K
+    1000-token sentences; oracle goldens over 3 seeds).
 The gate is one-sided: the parallel GPU dynamics score above the sequential
 reference on these corpora, and a higher score is not a defect. The deltas are
 printed (pytest -s) and recorded in DESIGN.md."""
@@ -25,6 +25,7 @@ from word2vec_amd.model import Word2Vec
 pytestmark = pytest.mark.gpu
 GOLD = json.loads((Path(__file__).parent / "golden" / "quality_oracle.json").read_text())
 ZGOLD = json.loads((Path(__file__).parent / "golden" / "quality_zipf_oracle.json").read_text())
+ZGOLD_CBOW_HS = json.loads((Path(__file__).parent / "golden" / "quality_zipf_cbow_hs_oracle.json").read_text())
 SENTS, QS, PAIRS = planted_corpus(**CORPUS)
 
 
@@ -55,13 +56,21 @@ def test_quality_planted_not_below_oracle(mode):
     assert d[0] >= -1.0 and d[1] >= -1.0, (mode, got, ref)
 
 
-def test_quality_text8_like_not_below_oracle():
+@pytest.mark.parametrize("mode", ["sg_ns", "cbow_hs"])
+def test_quality_text8_like_not_below_oracle(mode):
+    """SG-NS (1 seed) and configs[1]'s CBOW-HS (3 seeds: its LDS-privatised
+    context rows and Huffman top nodes make it the mode the update policy
+    shapes most) against the oracle's 3-seed mean."""
     sents, qs, pairs = planted_zipf_corpus(**ZCORPUS)
-    words, E = train_gpu(sents, "sg_ns", 11, ZTRAIN["iters"], ZTRAIN["dim"], ZTRAIN["table_size"],
-                         ZTRAIN["min_count"], ZTRAIN["subsample"])
-    got = np.array([analogy_accuracy(words, E, qs)["accuracy"], similarity_score(words, E, pairs)["spearman"]])
-    ref = np.array([[r["analogy"], r["similarity"]] for r in ZGOLD["scores"]]).mean(0)
-    print(f"text8-like sg_ns: gpu {got.round(2)} oracle {ref.round(2)} delta {(got - ref).round(2)}")
+    gold = ZGOLD if mode == "sg_ns" else ZGOLD_CBOW_HS
+    got = []
+    for seed in (11,) if mode == "sg_ns" else (11, 12, 13):
+        words, E = train_gpu(sents, mode, seed, ZTRAIN["iters"], ZTRAIN["dim"], ZTRAIN["table_size"],
+                             ZTRAIN["min_count"], ZTRAIN["subsample"])
+        got.append([analogy_accuracy(words, E, qs)["accuracy"], similarity_score(words, E, pairs)["spearman"]])
+    got = np.array(got).mean(0)
+    ref = np.array([[r["analogy"], r["similarity"]] for r in gold["scores"]]).mean(0)
+    print(f"text8-like {mode}: gpu {got.round(2)} oracle {ref.round(2)} delta {(got - ref).round(2)}")
     assert got[0] >= ref[0] - 1.0 and got[1] >= ref[1] - 1.0
 
 
@@ -88,7 +97,10 @@ def test_quality_shared_negatives_not_below_oracle(corpus):
         sents, qs, pairs = planted_zipf_corpus(**ZCORPUS)
         args = (ZTRAIN["iters"], ZTRAIN["dim"], ZTRAIN["table_size"], ZTRAIN["subsample"])
         ref = np.array([[r["analogy"], r["similarity"]] for r in ZGOLD["scores"]]).mean(0)
-    words, E = train(sents, *args, 11)
-    got = np.array([analogy_accuracy(words, E, qs)["accuracy"], similarity_score(words, E, pairs)["spearman"]])
+    got = []
+    for seed in (11, 12, 13):  # the gate is on means (the parallel schedule is not deterministic)
+        words, E = train(sents, *args, seed)
+        got.append([analogy_accuracy(words, E, qs)["accuracy"], similarity_score(words, E, pairs)["spearman"]])
+    got = np.array(got).mean(0)
     print(f"shared-negatives {corpus}: gpu {got.round(2)} oracle(per-pair) {ref.round(2)} delta {(got - ref).round(2)}")
     assert got[0] >= ref[0] - 1.0 and got[1] >= ref[1] - 1.0

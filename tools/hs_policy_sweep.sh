@@ -1,5 +1,5 @@
 # CBOW-HS d200 (configs[1] shape) throughput vs update policy knobs on one GPU.
-# usage (GPU box): bash tools/hs_policy_sweep.sh [extra bench args]
+# usage (GPU box): bash tools/hs_policy_sweep.sh
 mkdir -p gpurun_out
 run() {  # name, args...
   local n=$1; shift
@@ -10,10 +10,10 @@ run() {  # name, args...
   python -c "import json;d=json.load(open('gpurun_out/hs_$n.json'));print('$n', round(d['value']/1e6,1), 'M words/s', d['roofline']['avg_launch_ms'],'ms')"
 }
 run default
-run hot200 --hot-rows 200
-run hot64 --hot-rows 64
+run ctx_off --context-rows 0
+run ctx_flush16 --context-flush 16
+run ctx_flush256 --context-flush 256
+run ctx_flush1024 --context-flush 1024
 run hot0 --hot-rows 0
-run flush64 --flush-centers 64
-run flush256 --flush-centers 256
-run hot64_flush64 --hot-rows 64 --flush-centers 64
-run hogwild --hot-rows 0 --private-rows 0
+run cbow_ns_default --mode cbow_ns --dim 200 --negative 5
+run cbow_ns_ctx_off --mode cbow_ns --dim 200 --negative 5 --context-rows 0

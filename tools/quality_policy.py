@@ -1,7 +1,7 @@
 """Planted-corpus quality (the tests/test_gpu_quality.py gate: 3 seeds, mean
 delta vs the sequential oracle golden) per mode under alternative update
 policies, to pick per-mode defaults that keep the gate with the most speed.
-usage: python tools/quality_policy.py [mode ...]"""
+usage: python tools/quality_policy.py [mode ...] [policy=NAME ...]"""
 import sys
 from pathlib import Path
 
@@ -20,12 +20,22 @@ from word2vec_amd.model import Word2Vec  # noqa: E402
 GOLD = json.loads((ROOT / "tests" / "golden" / "quality_oracle.json").read_text())
 SENTS, QS, PAIRS = planted_corpus(**CORPUS)
 POLICIES = [("default", {}), ("hot_rows=0", dict(hot_rows=0)), ("hot_rows=64", dict(hot_rows=64)),
-            ("private off", dict(private_rows=0)), ("plain Hogwild", dict(hot_rows=0, private_rows=0))]
+            ("private off", dict(private_rows=0)), ("plain Hogwild", dict(hot_rows=0, private_rows=0, context_rows=0))]
+CBOW_POLICIES = [("context rows off", dict(context_rows=0)), ("context flush 16", dict(context_flush=16)),
+                 ("context flush 256", dict(context_flush=256)), ("context flush 1024", dict(context_flush=1024)),
+                 ("context only", dict(private_rows=0)), ("context only flush 64", dict(private_rows=0, context_flush=64)),
+                 ("both flush 64", dict(flush_centers=64, context_flush=64)),
+                 ("both flush 16", dict(flush_centers=16, context_flush=16)),
+                 ("context avg 1", dict(private_average=1.0)), ("context flush 32", dict(context_flush=32))]
+ONLY = [p for p in sys.argv[1:] if p.startswith("policy=")]
 
-for mode in sys.argv[1:] or list(MODES):
+for mode in [a for a in sys.argv[1:] if a in MODES] or list(MODES):
     m = MODES[mode]
     ref = np.array([[r["analogy"], r["similarity"]] for r in GOLD["scores"][mode]]).mean(0)
-    for name, pol in POLICIES:
+    pols = POLICIES + (CBOW_POLICIES if mode.startswith("cbow") else [])
+    if ONLY:
+        pols = [p for p in pols if f"policy={p[0]}" in ONLY]
+    for name, pol in pols:
         got = []
         for s in (11, 12, 13):
             w = Word2Vec(iter=ITERS[mode], window=5, min_count=TRAIN["min_count"], table_size=TRAIN["table_size"],

@@ -89,6 +89,7 @@ SIGNATURES = {
     "w2v_dev_set_hot_rows": (C.c_int, [_P, _I64]),
     "w2v_dev_set_private_rows": (C.c_int, [_P, _I32]),
     "w2v_dev_set_private_sync": (C.c_int, [_P, _I32, _F]),
+    "w2v_dev_set_context_private": (C.c_int, [_P, _I32, _I32]),
     "w2v_dev_set_max_waves": (C.c_int, [_P, _I64]),
     "w2v_dev_set_update": (C.c_int, [_P, _I32]),
     "w2v_dev_apply_rows": (C.c_int, [_P, _P, _P, _I32, _P, _P, _F, _I32]),

@@ -71,6 +71,8 @@ struct w2v_dev {
   int32_t private_rows = -1;  // hottest output rows privatised in LDS: -1 = auto, 0 = off
   int32_t flush_centers = 0;  // workgroup centers between flushes of the privatised rows (0 = auto)
   float private_average = 8.0f;  // concurrency the privatised rows' summed deltas are scaled to (0 = plain sum)
+  int32_t context_rows = -1;  // CBOW: hottest context rows privatised in LDS too: -1 = auto, 0 = off
+  int32_t context_flush = 0;  // workgroup centers between flushes of the context rows (0 = auto)
   int64_t max_waves = 0;      // cap on concurrently scheduled wavefronts (0 = as many as fit)
   bool need_C = false, need_S = false;
   float* W = nullptr;
@@ -549,31 +551,50 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   a.flush_every = h->flush_centers > 0 ? h->flush_centers : (h->cfg.hs ? 16 : 256);
   a.priv_avg = h->private_average;
   // LDS privatisation of the output layer's hottest rows (the NS target matrix
-  // — C for skip-gram, W for CBOW — or the top of the Huffman tree for HS):
-  // as many rows as fit 10 KiB per wave of the workgroup, <= 64 (the dirty mask).
+  // — C for skip-gram, W for CBOW — or the top of the Huffman tree for HS)
+  // and, for CBOW, of the hottest context rows of C (contexts are not
+  // subsampled: the most frequent words sit in most windows): as many rows as
+  // fit 10 KiB per wave of the workgroup, <= 64 per range (the dirty masks),
+  // the output rows first. Layout: lds_header_words in w2v_kernels.hpp.
   size_t lds_bytes = 0;
   a.priv_M = nullptr;
   a.priv_lo = 0;
   a.priv_n = 0;
-  {
+  a.ctx_M = nullptr;
+  a.ctx_n = 0;
+  a.ctx_flush_every = h->context_flush > 0 ? h->context_flush : (h->cfg.hs ? 32 : 256);
+  if (h->sched == W2V_SCHED_PARALLEL) {  // the reference-exact schedule keeps per-update rounding
     const int64_t row_bytes = (int64_t)h->nv * w2v::kWave * (int64_t)sizeof(float);
-    const int64_t budget = std::min<int64_t>(160 * 1024, 10 * 1024 * (int64_t)wpb) - 16 - 4 * 64;
+    const int64_t budget = std::min<int64_t>(160 * 1024, 10 * 1024 * (int64_t)wpb) - 4 * 136;
     int64_t fit = budget / row_bytes;
-    if (fit > 64) fit = 64;
-    int64_t P = h->private_rows < 0 ? fit : (h->private_rows < fit ? h->private_rows : fit);
+    int64_t P = std::min<int64_t>(fit, 64);
+    if (h->private_rows >= 0) P = std::min<int64_t>(P, h->private_rows);
     const bool hs = h->cfg.hs != 0;
     const int64_t avail = hs ? h->V - 1 : h->V;
     if (P > avail) P = avail;
-    if (h->sched == W2V_SCHED_SEQUENTIAL) P = 0;  // the reference-exact schedule keeps per-update rounding
     if (P > 0) {
       a.priv_M = hs ? h->S : (h->cfg.cbow ? h->W : h->C);
       a.priv_lo = hs ? avail - P : 0;  // HS: the P internal nodes nearest the root (V-2)
       a.priv_n = (int32_t)P;
-      lds_bytes = (size_t)(P * row_bytes) + 16 + (size_t)P * 4;  // + mask, counts, per-row hits
     }
+    // Auto: CBOW-HS only. It doubles CBOW-HS throughput and raises its planted-
+    // corpus scores; for CBOW-NS (hot rows privatised on both sides of every
+    // dot product) it fails the similarity gate at every flush interval tried
+    // (profiles/r01_context_rows.log).
+    int64_t Q = h->cfg.cbow ? std::min<int64_t>({fit - P, (int64_t)64, h->V}) : 0;
+    if (h->context_rows < 0 && !h->cfg.hs) Q = 0;
+    if (h->context_rows >= 0) Q = std::min<int64_t>(Q, h->context_rows);
+    if (Q > 0) {
+      a.ctx_M = h->C;
+      a.ctx_n = (int32_t)Q;
+    }
+    if (P + Q > 0)
+      lds_bytes = (size_t)(w2v::lds_header_words(P, Q) * (int64_t)sizeof(float) + (P + Q) * row_bytes);
   }
   if (sn_fn) {  // shared-negatives minibatch: 2-wave workgroups, static LDS
     a.priv_M = nullptr;
+    a.ctx_M = nullptr;
+    a.ctx_n = 0;
     a.item0 = 0;
     // LDS-private C rows (kSnPriv in w2v_shared.hpp: 16 KiB of rows, <= 32),
     // parallel schedule only, written back every flush_centers centers. Off
@@ -706,6 +727,15 @@ int w2v_dev_set_private_rows(w2v_dev* h, int32_t n) {
   if (!h) return fail(W2V_ERR_ARG, "null handle");
   if (n < -1) return fail(W2V_ERR_ARG, "private_rows must be >= -1");
   h->private_rows = n;
+  return W2V_OK;
+}
+
+int w2v_dev_set_context_private(w2v_dev* h, int32_t rows, int32_t flush_centers) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (rows < -1) return fail(W2V_ERR_ARG, "context rows must be >= -1");
+  if (flush_centers < 0) return fail(W2V_ERR_ARG, "flush_centers must be >= 0");
+  h->context_rows = rows;
+  h->context_flush = flush_centers;
   return W2V_OK;
 }
 

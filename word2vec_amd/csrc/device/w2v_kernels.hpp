@@ -91,6 +91,9 @@ struct TrainArgs {
   int32_t priv_n;
   float priv_avg;              // > 0: average, not sum, the workgroups' deltas of a privatised row (see flush_private)
   int32_t flush_every;         // the privatised deltas are flushed every this many centers of the workgroup
+  const float* ctx_M;          // CBOW: context matrix whose rows [0, ctx_n) are privatised too (or null)
+  int32_t ctx_n;
+  int32_t ctx_flush_every;     // centers of the workgroup between flushes of the context rows
   int64_t item0;               // shared-negatives kernel: work items are order[item0 + k] (or item0 + k)
 };
 
@@ -160,6 +163,59 @@ __device__ __forceinline__ uint32_t philox_table_pos(const TrainArgs& a, uint32_
 }
 
 // ---------------------------------------------------------------------------
+// LDS-privatised rows of the per-pair kernel (when priv_n + ctx_n > 0), per workgroup:
+//   words [0,1] dirty mask of the output rows, [2,3] of the context rows,
+//   [4] centers of the workgroup, [5] / [6] flushes of either range, [7] unused,
+//   [8, 8 + priv_n) and [8 + priv_n, 8 + priv_n + ctx_n) per-row flush hits,
+//   then (from lds_header_words) the pending deltas: priv_n output rows, then
+//   ctx_n context rows, NV * 64 floats each.
+// ---------------------------------------------------------------------------
+__host__ __device__ inline int64_t lds_header_words(int64_t priv_n, int64_t ctx_n) {
+  return (8 + priv_n + ctx_n + 3) & ~int64_t(3);
+}
+
+struct PrivRows {  // one privatised row range [lo, lo + n) of matrix M (n == 0: none)
+  float* delta = nullptr;
+  unsigned long long* dirty = nullptr;
+  unsigned* flushes = nullptr;
+  unsigned* hits = nullptr;
+  float* M = nullptr;
+  int64_t lo = 0;
+  int n = 0;
+  __device__ bool has(int64_t row) const { return row >= lo && row < lo + n; }
+};
+
+template <int NV>
+__device__ __forceinline__ PrivRows out_rows(const TrainArgs& a, float* lds) {
+  PrivRows p;
+  if (lds == nullptr || a.priv_n == 0) return p;
+  unsigned* u = reinterpret_cast<unsigned*>(lds);
+  p.dirty = reinterpret_cast<unsigned long long*>(lds);
+  p.flushes = u + 5;
+  p.hits = u + 8;
+  p.delta = lds + lds_header_words(a.priv_n, a.ctx_n);
+  p.M = const_cast<float*>(a.priv_M);
+  p.lo = a.priv_lo;
+  p.n = a.priv_n;
+  return p;
+}
+
+template <int NV>
+__device__ __forceinline__ PrivRows ctx_rows(const TrainArgs& a, float* lds) {
+  PrivRows p;
+  if (lds == nullptr || a.ctx_n == 0) return p;
+  unsigned* u = reinterpret_cast<unsigned*>(lds);
+  p.dirty = reinterpret_cast<unsigned long long*>(lds + 2);
+  p.flushes = u + 6;
+  p.hits = u + 8 + a.priv_n;
+  p.delta = lds + lds_header_words(a.priv_n, a.ctx_n) + (int64_t)a.priv_n * (NV * kWave);
+  p.M = const_cast<float*>(a.ctx_M);
+  p.lo = 0;
+  p.n = a.ctx_n;
+  return p;
+}
+
+// ---------------------------------------------------------------------------
 // Row I/O: a row is NV floats per lane, element lane + 64 v (v < NV).
 // ---------------------------------------------------------------------------
 template <int NV>
@@ -213,6 +269,26 @@ __device__ __forceinline__ void add_to_row(float* M, int64_t row, bool hot, int6
   }
 }
 
+// A privatised row's value is the global row plus this workgroup's pending delta.
+template <int NV>
+__device__ __forceinline__ void priv_read(const PrivRows& pr, int64_t row, int lane, float (&r)[NV]) {
+  const float* q = pr.delta + (row - pr.lo) * (NV * kWave) + lane;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) r[v] += q[kWave * v];
+}
+
+// ds_add_f32 of delta into the row's pending delta, then mark the row dirty
+// (after the adds: a wave's LDS operations are ordered).
+template <int NV>
+__device__ __forceinline__ void priv_add(const PrivRows& pr, int64_t row, int d, int lane, const float (&delta)[NV]) {
+  const int64_t p = row - pr.lo;
+  float* q = pr.delta + p * (NV * kWave) + lane;
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+    if (lane + kWave * v < d) atomicAdd(q + kWave * v, delta[v]);
+  if (lane == 0) atomicOr(pr.dirty, 1ull << p);
+}
+
 // ---------------------------------------------------------------------------
 // The per-target update (Word2Vec.cpp:238-246 HS; :261-268 NS), for up to
 // MAXT distinct rows at once. Lane (t0 + t) of row_l / code_l holds target t's
@@ -223,24 +299,21 @@ __device__ __forceinline__ void add_to_row(float* M, int64_t row, bool hot, int6
 template <int NV, int MAXT, bool HSF>
 __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, int lane, int T, int row_l,
                                               int code_l, int t0, const float (&x)[NV], float (&g)[NV],
-                                              float alpha, int64_t hot_lo, int64_t hot_hi, float* lds,
-                                              int64_t priv_lo, int64_t priv_n) {
+                                              float alpha, int64_t hot_lo, int64_t hot_hi, const PrivRows& pr) {
   float r[MAXT][NV];
   int rows[MAXT];
   bool hot[MAXT], priv[MAXT];
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) {
     rows[t] = readlane_i(row_l, t0 + t);
-    priv[t] = lds != nullptr && rows[t] >= priv_lo && rows[t] < priv_lo + priv_n;
+    priv[t] = pr.has(rows[t]);
     hot[t] = !priv[t] && rows[t] >= hot_lo && rows[t] < hot_hi;
     if (t < T) load_row<NV>(M, rows[t], pitch, d, lane, hot[t] || priv[t], r[t]);
   }
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) {  // privatised rows: global value + this workgroup's pending delta
     if (t < T && priv[t]) {
-      const float* q = lds + (rows[t] - priv_lo) * (NV * kWave) + lane;
-#pragma unroll
-      for (int v = 0; v < NV; ++v) r[t][v] += q[kWave * v];
+      priv_read<NV>(pr, rows[t], lane, r[t]);
     }
   }
   float f[MAXT];
@@ -274,13 +347,7 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
         delta[v] = gt * x[v];
       }
       if (priv[t]) {  // ds_add_f32 into the workgroup's delta; flushed after the center
-        const int64_t pr = rows[t] - priv_lo;
-        float* q = lds + pr * (NV * kWave) + lane;
-#pragma unroll
-        for (int v = 0; v < NV; ++v)
-          if (lane + kWave * v < d) atomicAdd(q + kWave * v, delta[v]);
-        if (lane == 0)  // after the adds (a wave's LDS ops are ordered): mark the row dirty
-          atomicOr(reinterpret_cast<unsigned long long*>(lds + priv_n * (NV * kWave)), 1ull << pr);
+        priv_add<NV>(pr, rows[t], d, lane, delta);
       } else if (hot[t]) {
         atomic_add_row<NV>(M, rows[t], pitch, d, lane, delta);
       } else {
@@ -298,12 +365,10 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
 // workgroup is neither lost nor flushed twice (its dirty bit is set after its
 // adds and survives until the next flush).
 template <int NV>
-__device__ __forceinline__ void flush_private(const TrainArgs& a, float* lds, int lane) {
-  if (lds == nullptr) return;
-  unsigned long long* dirty = reinterpret_cast<unsigned long long*>(lds + a.priv_n * (NV * kWave));
-  unsigned* tail = reinterpret_cast<unsigned*>(dirty);  // [0,1] dirty mask, [2] centers, [3] flushes, [4+p] hits
+__device__ __forceinline__ void flush_private(const TrainArgs& a, const PrivRows& pr, int lane) {
+  if (pr.n == 0) return;
   unsigned long long m = 0;
-  if (lane == 0) m = atomicExch(dirty, 0ull);
+  if (lane == 0) m = atomicExch(pr.dirty, 0ull);
   m = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(m >> 32)) << 32) |
       (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)m);
   if (m == 0) return;
@@ -314,23 +379,22 @@ __device__ __forceinline__ void flush_private(const TrainArgs& a, float* lds, in
   float flushes = 1.0f;
   if (a.priv_avg > 0.0f) {
     unsigned fl = 0;
-    if (lane == 0) fl = atomicAdd(tail + 3, 1u) + 1u;
+    if (lane == 0) fl = atomicAdd(pr.flushes, 1u) + 1u;
     flushes = (float)(unsigned)__builtin_amdgcn_readfirstlane((int)fl);
   }
-  float* M = const_cast<float*>(a.priv_M);
   while (m) {
     const int p = __builtin_ctzll(m);
     m &= m - 1;
     float sc = 1.0f;
     if (a.priv_avg > 0.0f) {
       unsigned h = 0;
-      if (lane == 0) h = atomicAdd(tail + 4 + p, 1u) + 1u;
+      if (lane == 0) h = atomicAdd(pr.hits + p, 1u) + 1u;
       const float hits = (float)(unsigned)__builtin_amdgcn_readfirstlane((int)h);
       const float n = (float)gridDim.x * hits / flushes;
       sc = 1.0f / fmaxf(1.0f, n / a.priv_avg);
     }
-    float* q = lds + p * (NV * kWave) + lane;
-    float* dst = M + (a.priv_lo + p) * a.pitch + lane;
+    float* q = pr.delta + p * (NV * kWave) + lane;
+    float* dst = pr.M + (pr.lo + p) * a.pitch + lane;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       if (lane + kWave * v < a.dim) {
@@ -346,7 +410,7 @@ __device__ __forceinline__ void flush_private(const TrainArgs& a, float* lds, in
 template <int NV, int MAXT>
 __device__ __forceinline__ void hs_word(const TrainArgs& a, int word, int lane, const float (&x)[NV],
                                         float (&g)[NV], float alpha, Counters& cnt, float* lds) {
-  float* plds = (a.priv_M == a.S) ? lds : nullptr;
+  const PrivRows pr = (a.priv_M == a.S) ? out_rows<NV>(a, lds) : PrivRows();
   const int64_t cb = a.coff[word];
   const int L = (int)(a.coff[word + 1] - cb);
   for (int c0 = 0; c0 < L; c0 += kWave) {
@@ -356,7 +420,7 @@ __device__ __forceinline__ void hs_word(const TrainArgs& a, int word, int lane, 
     for (int t0 = 0; t0 < rem; t0 += MAXT) {
       if (a.strict) drain_vmem();
       apply_targets<NV, MAXT, true>(a.S, a.pitch, a.dim, lane, min(MAXT, rem - t0), pt_l, cd_l, t0, x, g,
-                                    alpha, a.hot_s, INT64_MAX, plds, a.priv_lo, a.priv_n);
+                                    alpha, a.hot_s, INT64_MAX, pr);
     }
     cnt.targets += (unsigned long long)rem;
   }
@@ -369,7 +433,7 @@ template <int NV, int MAXT>
 __device__ __forceinline__ void ns_word(const TrainArgs& a, float* M, int word, int negw_l, int base, int lane,
                                         const float (&x)[NV], float (&g)[NV], float alpha, Counters& cnt,
                                         float* lds) {
-  float* plds = (a.priv_M == M) ? lds : nullptr;
+  const PrivRows pr = (a.priv_M == M) ? out_rows<NV>(a, lds) : PrivRows();
   const int neg = a.negative;
   const int nk = __shfl(negw_l, (base + lane) & (kWave - 1));
   bool dup = (lane >= neg) || (nk == word);
@@ -392,7 +456,7 @@ __device__ __forceinline__ void ns_word(const TrainArgs& a, float* M, int word, 
   for (int t0 = 0; t0 < T; t0 += MAXT) {
     if (a.strict) drain_vmem();
     apply_targets<NV, MAXT, false>(M, a.pitch, a.dim, lane, min(MAXT, T - t0), tgt_l, code_l, t0, x, g, alpha,
-                                   0, a.hot_wc, plds, a.priv_lo, a.priv_n);
+                                   0, a.hot_wc, pr);
   }
   cnt.targets += (unsigned long long)T;
 }
@@ -502,6 +566,7 @@ __device__ __forceinline__ void cbow_center(const TrainArgs& a, float* lds, cons
   float h[NV], g[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) h[v] = g[v] = 0.f;
+  const PrivRows cx = ctx_rows<NV>(a, lds);  // the hottest context rows: global value + pending delta
   if (a.strict) drain_vmem();
   for (int r0 = 0; r0 < U; r0 += MAXT) {
     float rr[MAXT][NV];
@@ -509,11 +574,13 @@ __device__ __forceinline__ void cbow_center(const TrainArgs& a, float* lds, cons
     for (int t = 0; t < MAXT; ++t)
       if (r0 + t < U) {
         const int row = readlane_i(sid, r0 + t);
-        load_row<NV>(a.C, row, a.pitch, a.dim, lane, row < a.hot_wc, rr[t]);
+        load_row<NV>(a.C, row, a.pitch, a.dim, lane, row < a.hot_wc || cx.has(row), rr[t]);
       }
 #pragma unroll
     for (int t = 0; t < MAXT; ++t)
       if (r0 + t < U) {
+        const int row = readlane_i(sid, r0 + t);
+        if (cx.has(row)) priv_read<NV>(cx, row, lane, rr[t]);
 #pragma unroll
         for (int v = 0; v < NV; ++v) h[v] += rr[t][v];
       }
@@ -536,7 +603,10 @@ __device__ __forceinline__ void cbow_center(const TrainArgs& a, float* lds, cons
   }
   for (int r = 0; r < U; ++r) {  // C.row(id) += neu1_grad for every unique id (:315)
     const int row = readlane_i(sid, r);
-    add_to_row<NV>(a.C, row, row < a.hot_wc, a.pitch, a.dim, lane, g);
+    if (cx.has(row))
+      priv_add<NV>(cx, row, a.dim, lane, g);
+    else
+      add_to_row<NV>(a.C, row, row < a.hot_wc, a.pitch, a.dim, lane, g);
   }
 }
 
@@ -553,11 +623,12 @@ __device__ __forceinline__ void center(const TrainArgs& a, float* lds, const int
     // center count, and the wave that completes every flush_every-th center
     // drains the deltas all of them accumulated (one atomic per dirty row
     // instead of one per update and wave).
-    unsigned* done = reinterpret_cast<unsigned*>(lds + a.priv_n * (NV * kWave) + 2);
+    unsigned* done = reinterpret_cast<unsigned*>(lds) + 4;
     unsigned n = 0;
     if (lane == 0) n = atomicAdd(done, 1u) + 1u;
     n = (unsigned)__builtin_amdgcn_readfirstlane((int)n);
-    if (n % (unsigned)a.flush_every == 0u) flush_private<NV>(a, lds, lane);
+    if (a.priv_n > 0 && n % (unsigned)a.flush_every == 0u) flush_private<NV>(a, out_rows<NV>(a, lds), lane);
+    if (a.ctx_n > 0 && n % (unsigned)a.ctx_flush_every == 0u) flush_private<NV>(a, ctx_rows<NV>(a, lds), lane);
   }
 }
 
@@ -568,9 +639,10 @@ template <int NV, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY>
 __global__ __launch_bounds__(kMaxBlock<NV>) void train_epoch_kernel(TrainArgs a) {
   extern __shared__ float w2v_lds[];
   const int lane = lane_id();
-  float* lds = a.priv_n > 0 ? w2v_lds : nullptr;
+  float* lds = (a.priv_n + a.ctx_n) > 0 ? w2v_lds : nullptr;
   if (lds) {
-    for (int k = threadIdx.x; k < a.priv_n * (NV * kWave + 1) + 4; k += blockDim.x) lds[k] = 0.0f;  // deltas + tail
+    const int64_t words = lds_header_words(a.priv_n, a.ctx_n) + (int64_t)(a.priv_n + a.ctx_n) * (NV * kWave);
+    for (int64_t k = threadIdx.x; k < words; k += blockDim.x) lds[k] = 0.0f;
     __syncthreads();
   }
   Counters cnt;
@@ -630,7 +702,8 @@ __global__ __launch_bounds__(kMaxBlock<NV>) void train_epoch_kernel(TrainArgs a)
     if (lane == 0) atomicAdd(a.words, (unsigned long long)len);
     cnt.sentences += 1;
   }
-  flush_private<NV>(a, lds, lane);
+  flush_private<NV>(a, out_rows<NV>(a, lds), lane);
+  flush_private<NV>(a, ctx_rows<NV>(a, lds), lane);
   if (lane == 0) {
     atomicAdd(&a.stats[0], cnt.centers);
     atomicAdd(&a.stats[1], cnt.contexts);
@@ -657,9 +730,9 @@ __global__ __launch_bounds__(64) void apply_rows_kernel(float* M, int64_t pitch,
   for (int t = 0; t < n; ++t) {
     const int code = (int)codes[t];
     if (hs_form)
-      apply_targets<NV, 1, true>(M, pitch, d, lane, 1, t, code, 0, x, g, alpha, 0, 0, nullptr, 0, 0);
+      apply_targets<NV, 1, true>(M, pitch, d, lane, 1, t, code, 0, x, g, alpha, 0, 0, PrivRows());
     else
-      apply_targets<NV, 1, false>(M, pitch, d, lane, 1, t, code, 0, x, g, alpha, 0, 0, nullptr, 0, 0);
+      apply_targets<NV, 1, false>(M, pitch, d, lane, 1, t, code, 0, x, g, alpha, 0, 0, PrivRows());
   }
 #pragma unroll
   for (int v = 0; v < NV; ++v) {

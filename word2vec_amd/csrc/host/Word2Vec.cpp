@@ -343,6 +343,7 @@ void Word2Vec::run_epochs(const std::vector<int32_t>& ids, const std::vector<int
   check(w2v_dev_set_private_rows(dev_, private_rows), "w2v_dev_set_private_rows");
   check(w2v_dev_set_private_sync(dev_, flush_centers, private_average), "w2v_dev_set_private_sync");
   check(w2v_dev_set_max_waves(dev_, max_waves), "w2v_dev_set_max_waves");
+  check(w2v_dev_set_context_private(dev_, context_rows, context_flush), "w2v_dev_set_context_private");
   check(w2v_dev_set_update(dev_, shared_negatives ? W2V_UPDATE_SHARED_NEGATIVES : W2V_UPDATE_PER_PAIR),
         "w2v_dev_set_update");
   check(w2v_dev_set_progress(dev_, 0), "w2v_dev_set_progress");  // current_words = 0 (:359)

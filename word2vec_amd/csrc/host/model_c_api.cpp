@@ -82,6 +82,11 @@ void w2v_model_update_policy(w2v_model* m, int64_t hot_rows, int32_t private_row
   m->w.max_waves = max_waves;
 }
 
+void w2v_model_context_policy(w2v_model* m, int32_t context_rows, int32_t context_flush) {
+  m->w.context_rows = context_rows;
+  m->w.context_flush = context_flush;
+}
+
 void w2v_model_set_shared_negatives(w2v_model* m, int32_t on) { m->w.shared_negatives = on != 0; }
 
 int w2v_model_build_vocab(w2v_model* m, const char* text, int64_t len) {

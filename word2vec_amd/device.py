@@ -186,6 +186,12 @@ class DeviceTrainer:
         self._chk(self.lib.w2v_dev_set_private_sync(self.h, int(flush_centers), float(average_over)),
                   "w2v_dev_set_private_sync")
 
+    def set_context_private(self, rows: int = -1, flush_centers: int = 0):
+        """CBOW: hottest context rows privatised in LDS too (-1 auto, 0 off) and the
+        workgroup centers between their flushes (0 = auto); include/w2v_dev.h."""
+        self._chk(self.lib.w2v_dev_set_context_private(self.h, int(rows), int(flush_centers)),
+                  "w2v_dev_set_context_private")
+
     def set_max_waves(self, n: int):
         """Cap on wavefronts in flight (0 = as many as fit)."""
         self._chk(self.lib.w2v_dev_set_max_waves(self.h, int(n)), "w2v_dev_set_max_waves")

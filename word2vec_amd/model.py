@@ -30,6 +30,7 @@ def _load():
             "w2v_model_seed": (None, [P, C.c_uint32]),
             "w2v_model_options": (None, [P, I32, I32, I32]),
             "w2v_model_update_policy": (None, [P, I64, I32, I32, F, I64]),
+            "w2v_model_context_policy": (None, [P, I32, I32]),
             "w2v_model_set_shared_negatives": (None, [P, I32]),
             "w2v_model_build_vocab": (C.c_int, [P, S, I64]),
             "w2v_model_train": (C.c_int, [P, S, I64]),
@@ -81,7 +82,8 @@ class Word2Vec:
     def __init__(self, iter=1, window=5, min_count=5, table_size=100_000_000, word_dim=200, negative=0,
                  subsample_threshold=0.001, init_alpha=0.025, min_alpha=1e-6, cbow_mean=False, num_threads=1,
                  train_method="hs", model="cbow", gpu_device=0, replay_rng=False, verbose=False, hot_rows=1000,
-                 private_rows=-1, flush_centers=0, private_average=8.0, max_waves=0, shared_negatives=False):
+                 private_rows=-1, flush_centers=0, private_average=8.0, max_waves=0, shared_negatives=False,
+                 context_rows=-1, context_flush=0):
         self.L = _load()
         self.word_dim = word_dim
         self.h = self.L.w2v_model_new(iter, window, min_count, table_size, word_dim, negative, subsample_threshold,
@@ -93,6 +95,7 @@ class Word2Vec:
         self.L.w2v_model_update_policy(self.h, int(hot_rows), int(private_rows), int(flush_centers),
                                        float(private_average), int(max_waves))
         self.L.w2v_model_set_shared_negatives(self.h, int(bool(shared_negatives)))
+        self.L.w2v_model_context_policy(self.h, int(context_rows), int(context_flush))
 
     def __del__(self):
         try:
