@@ -201,7 +201,11 @@ int w2v_dev_set_max_waves(w2v_dev* h, int64_t n);
  * rows), and the window's updates are the three GEMMs L = W_in C_out^T,
  * dW_in = E C_out, dC_out = E^T W_in on the matrix cores. Skip-gram NS only,
  * negative <= 15, window <= 8, Philox draws, row pitch 64 * {1..8,10,12,14,16}
- * floats (W2V_ERR_UNSUPPORTED otherwise). */
+ * floats (W2V_ERR_UNSUPPORTED otherwise). Its parallel-schedule policy:
+ * rows below hot_rows add their deltas with memory-side atomics, frequent
+ * rows are read and written device-coherently, and private_rows (auto: <= 4)
+ * of the hottest C rows are privatised per workgroup, flushed every
+ * flush_centers (auto: 1024) centers. */
 int w2v_dev_set_update(w2v_dev* h, int32_t mode);
 
 /* Word2Vec::train_sentence_* take alpha from the caller (Word2Vec.h:83-84):

@@ -596,22 +596,29 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     a.ctx_M = nullptr;
     a.ctx_n = 0;
     a.item0 = 0;
-    // LDS-private C rows (kSnPriv in w2v_shared.hpp: 16 KiB of rows, <= 32),
-    // parallel schedule only, written back every flush_centers centers. Off
-    // unless private_rows > 0: measured on configs[4], 8 rows flushed every 64
-    // centers gain 12 % but cost 1.6 points of similarity on the text8-like
-    // gate, and every 16 centers gain nothing (profiles/r01_sn_private_sweep.log).
-    a.priv_n = h->sched == W2V_SCHED_PARALLEL && h->private_rows > 0
-                   ? (int32_t)std::min<int64_t>({(int64_t)32, 16384 / (h->pitch * (int64_t)sizeof(float)), h->V,
-                                                 (int64_t)h->private_rows})
-                   : 0;
-    a.flush_every = h->flush_centers > 0 ? h->flush_centers : 64;
+    // LDS row slots (kSnPriv in w2v_shared.hpp: 16 KiB of rows, <= 32), parallel
+    // schedule only. The first priv_n hold the workgroup's pending deltas of
+    // the hottest C rows, added to HBM with atomics every flush_centers centers
+    // (auto: half the slots, <= 4, every 1024 centers); the rest stage the
+    // atomic rows' deltas of each center. Measured on configs[4]: 4 private
+    // rows + staged atomics 72 M words/s vs 61 M with neither, and higher
+    // planted / text8-like scores (profiles/r01_sn_atomic_rows.log).
+    {
+      const int64_t slots = std::min<int64_t>(32, w2v::kSnPrivBytes / (h->pitch * (int64_t)sizeof(float)));
+      const int64_t want = h->private_rows < 0 ? std::min<int64_t>(4, slots / 2) : h->private_rows;
+      a.priv_n = h->sched == W2V_SCHED_PARALLEL ? (int32_t)std::min<int64_t>({slots, h->V, want}) : 0;
+    }
+    a.flush_every = h->flush_centers > 0 ? h->flush_centers : 1024;
     const int threads = sn_waves * w2v::kWave;
     // device-coherent rows (rows_rsrc in w2v_shared.hpp): all for hot_rows =
     // -1, else at least the rows two XCD L2s' capacity could keep resident
     const int64_t l2_rows = (int64_t)(8 << 20) / (h->pitch * (int64_t)sizeof(float));
     a.hot_wc = h->hot_rows < 0 ? h->V : std::min<int64_t>(h->V, std::max<int64_t>(h->hot_rows, l2_rows));
     if (const char* e = std::getenv("W2V_SN_COHERENT_ROWS")) a.hot_wc = std::min<int64_t>(h->V, std::atoll(e));  // experiments
+    // the hot_rows most frequent rows take atomic deltas, as in the per-pair
+    // kernel (parallel schedule only: the sequential one is exact either way)
+    a.hot_atomic = h->sched == W2V_SCHED_PARALLEL ? std::min<int64_t>(h->V, h->hot_rows < 0 ? h->V : h->hot_rows) : 0;
+    if (const char* e = std::getenv("W2V_SN_ATOMIC_ROWS")) a.hot_atomic = std::min<int64_t>(h->V, std::atoll(e));  // experiments
     int64_t g = 1;
     if (h->sched == W2V_SCHED_PARALLEL) {
       int per_cu = 0;

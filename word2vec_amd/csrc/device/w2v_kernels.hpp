@@ -95,7 +95,11 @@ struct TrainArgs {
   int32_t ctx_n;
   int32_t ctx_flush_every;     // centers of the workgroup between flushes of the context rows
   int64_t item0;               // shared-negatives kernel: work items are order[item0 + k] (or item0 + k)
+  int64_t hot_atomic;          // shared-negatives kernel: W / C rows [0, hot_atomic) take memory-side atomic deltas
 };
+
+// LDS the shared-negatives kernel gives its private C rows (w2v_shared.hpp kSnPriv; <= 32 rows).
+constexpr int kSnPrivBytes = 16 * 1024;
 
 struct Counters {
   unsigned long long centers = 0, contexts = 0, targets = 0, draws = 0, sentences = 0;

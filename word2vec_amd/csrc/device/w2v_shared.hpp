@@ -60,7 +60,7 @@ constexpr int kSnRing = 256;    // kept-token ring (holds a 64-center batch, its
 // on a handful of memory channels: measured, 16 coherent rows cost a third of
 // the throughput). P fills 16 KiB of LDS, at most 32 rows.
 template <int KB, int NW>
-constexpr int kSnPriv = (16384 / (NW * KB * 64)) < 32 ? (16384 / (NW * KB * 64)) : 32;
+constexpr int kSnPriv = (kSnPrivBytes / (NW * KB * 64)) < 32 ? (kSnPrivBytes / (NW * KB * 64)) : 32;
 
 template <int KB, int NW>
 struct SnShared {
@@ -164,7 +164,7 @@ __device__ __forceinline__ float sn_grad(float l, bool positive, float alpha) {
 template <int KB, int NW>
 __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<KB, NW>& sh, __amdgpu_buffer_rsrc_t rW,
                                           __amdgpu_buffer_rsrc_t rC, int wave, int lane, int t, int nk, int b,
-                                          float alpha, int& par, Counters& cnt, SnProf& pf_) {
+                                          float alpha, int& par, Counters& cnt, SnProf& pf_, unsigned& dirty) {
   pf_.stamp(0);
   const int q = lane >> 4, col = lane & 15;
   const int c = sh.ring_id[t & (kSnRing - 1)], rw = sh.ring_rw[t & (kSnRing - 1)];
@@ -201,6 +201,7 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<KB, NW>& 
   const int64_t cb = (int64_t)wave * (kSnTile * KB) + 4 * q;
   const uint32_t wo = (uint32_t)(((int64_t)in_row * a.pitch + cb) * 4);  // byte offsets (< 4 GiB, host-checked)
   const bool w_coh = in_row < a.hot_wc;
+  const bool w_atom = in_row < a.hot_atomic;
   if (a.strict) drain_vmem();  // sequential schedule: this wave's own stores land before the re-read
   f32x4 wr[KB], cr[KB];
 #pragma unroll
@@ -220,7 +221,16 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<KB, NW>& 
   const uint32_t co = (uint32_t)(((int64_t)out_row * a.pitch + cb) * 4);
   const bool c_coh = out_row < a.hot_wc;
   const bool c_priv = out_row < a.priv_n;  // this workgroup's pending delta lives in LDS
+  const bool c_atom = !c_priv && out_row < a.hot_atomic;
   float* pr = &sh.priv[c_priv ? out_row : 0][(int)cb];
+  if (a.priv_n > 0) {  // this wave's dirty private rows (lanes 0..15 hold the 16 output slots)
+    unsigned long long pm = ballot(c_priv && out_ok && lane < kSnTile);
+    while (pm) {
+      const int bb = __builtin_ctzll(pm);
+      pm &= pm - 1;
+      dirty |= 1u << readlane_i(out_row, bb);
+    }
+  }
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) cr[kb] = load_row4(rC, co + 64u * kb, c_coh);
   cnt.centers += 1;
@@ -276,6 +286,19 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<KB, NW>& 
     }
   }
   const int n_out = (K + 1 + 3) >> 2, n_in = (M + 3) >> 2;
+  // Atomic rows (below a.hot_atomic): their deltas are staged in the free
+  // private-row slots of LDS (this wave's columns) and added to HBM row-wise
+  // after the update, 256 contiguous bytes per atomic instruction; rows past
+  // the free slots fall back to the coherent store.
+  const int n_slots = kSnPriv<KB, NW> - a.priv_n;
+  const unsigned long long atw = ballot(w_atom && in_ok && lane < kSnTile);
+  const unsigned long long atc = ballot(c_atom && out_ok && lane < kSnTile);
+  const unsigned long long below = (1ull << col) - 1ull;
+  int w_slot = (w_atom && in_ok) ? __popcll(atw & below) : n_slots;
+  int c_slot = (c_atom && out_ok) ? __popcll(atw) + __popcll(atc & below) : n_slots;
+  const bool w_stage = w_slot < n_slots, c_stage = c_slot < n_slots;
+  float* ws = &sh.priv[a.priv_n + (w_stage ? w_slot : 0)][(int)cb];
+  float* cs = &sh.priv[a.priv_n + (c_stage ? c_slot : 0)][(int)cb];
   pf_.stamp(5);
   // dW^T = C^T E^T and dC^T = W^T E per 16-column block, added in place;
   // block kb + 1 goes into the other transpose buffer while kb is consumed
@@ -306,34 +329,68 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<KB, NW>& 
     wr[kb] += dw;
     cr[kb] += dc;
     if (c_priv && out_ok) *reinterpret_cast<f32x4*>(pr + kSnTile * kb) += dc;
+    if (w_stage) *reinterpret_cast<f32x4*>(ws + kSnTile * kb) = dw;
+    if (c_stage) *reinterpret_cast<f32x4*>(cs + kSnTile * kb) = dc;
     if (kb & 1) {  // blocks kb - 1, kb written back as whole 128-B lines
-      store_pair(wr[kb - 1], wr[kb], rW, wo + 64u * (kb - 1), in_ok, w_coh, col);
-      store_pair(cr[kb - 1], cr[kb], rC, co + 64u * (kb - 1), out_ok && !c_priv, c_coh, col);
+      store_pair(wr[kb - 1], wr[kb], rW, wo + 64u * (kb - 1), in_ok && !w_stage, w_coh, col);
+      store_pair(cr[kb - 1], cr[kb], rC, co + 64u * (kb - 1), out_ok && !c_priv && !c_stage, c_coh, col);
     }
+  }
+  {  // the staged atomic rows, row by row
+    constexpr int kCols = KB * kSnTile;
+    wave_lds_order();
+    unsigned long long mw = atw, mc = atc;
+    for (int sl = 0; sl < n_slots && (mw | mc); ++sl) {
+      const bool is_w = mw != 0;
+      const int bb = __builtin_ctzll(is_w ? mw : mc);
+      if (is_w) mw &= mw - 1; else mc &= mc - 1;
+      const int64_t row = readlane_i(is_w ? in_row : out_row, bb);
+      float* dst = (is_w ? a.W : a.C) + row * a.pitch + wave * kCols;
+      const float* src = &sh.priv[a.priv_n + sl][wave * kCols];
+#pragma unroll
+      for (int cc = 0; cc < kCols; cc += kWave)
+        if (cc + lane < kCols)
+          (void)__hip_atomic_fetch_add(dst + cc + lane, src[cc + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    wave_lds_order();
   }
   pf_.stamp(6);
 }
 
-// Write this wave's columns of the private rows' pending deltas back to C
-// (coherent read-modify-write, as every other frequent row) and clear them.
+// Move this wave's columns of its dirty private rows' pending deltas into C
+// with memory-side float atomics (no update lost between workgroups) and clear
+// them. As in the per-pair kernel's flush_private (w2v_kernels.hpp), with
+// priv_avg = S > 0 a row that n workgroups update within one flush interval
+// gets its delta scaled to at most S concurrent contributions, n = workgroups
+// x the fraction of this wave's flushes in which the row was dirty (hits_l:
+// lane r counts row r's).
 template <int KB, int NW>
-__device__ __forceinline__ void sn_flush_private(const TrainArgs& a, SnShared<KB, NW>& sh, __amdgpu_buffer_rsrc_t rC,
-                                                 int wave, int lane) {
+__device__ __forceinline__ void sn_flush_private(const TrainArgs& a, SnShared<KB, NW>& sh, int wave, int lane,
+                                                 unsigned& dirty, unsigned& flushes, unsigned& hits_l) {
   constexpr int kCols = KB * kSnTile;  // this wave's columns of a row
-  for (int r = 0; r < a.priv_n; ++r) {
-#pragma unroll
-    for (int c0 = 0; c0 < kCols; c0 += 4 * kWave) {
-      const int cc = c0 + 4 * lane;
-      if (cc < kCols) {
-        float* p = &sh.priv[r][wave * kCols + cc];
-        const f32x4 dlt = *reinterpret_cast<f32x4*>(p);
-        const uint32_t off = (uint32_t)(((int64_t)r * a.pitch + wave * kCols + cc) * 4);
-        const f32x4 v = load_row4(rC, off, true) + dlt;
-        store_row4(v, rC, off, true);
-        *reinterpret_cast<f32x4*>(p) = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
+  unsigned m = (unsigned)__builtin_amdgcn_readfirstlane((int)dirty);
+  dirty = 0;
+  if (m == 0) return;
+  flushes += 1;
+  if (lane < 32 && ((m >> lane) & 1u)) hits_l += 1;
+  wave_lds_order();
+  while (m) {
+    const int r = __builtin_ctz(m);
+    m &= m - 1;
+    float sc = 1.0f;
+    if (a.priv_avg > 0.0f) {
+      const float n = (float)gridDim.x * (float)(unsigned)readlane_i((int)hits_l, r) / (float)flushes;
+      sc = 1.0f / fmaxf(1.0f, n / a.priv_avg);
+    }
+    float* dst = a.C + (int64_t)r * a.pitch + wave * kCols;
+    for (int cc = lane; cc < kCols; cc += kWave) {
+      float* p = &sh.priv[r][wave * kCols + cc];
+      const float v = *p;
+      *p = 0.f;
+      if (v != 0.f) (void)__hip_atomic_fetch_add(dst + cc, v * sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  wave_lds_order();
 }
 
 // Epoch kernel: workgroups dequeue sentences (Word2Vec.cpp:375-394) and walk
@@ -351,6 +408,7 @@ __global__ __launch_bounds__(NW * kWave, WAVES_PER_SIMD) void train_shared_neg_k
   const __amdgpu_buffer_rsrc_t rW = rows_rsrc(a.W), rC = rows_rsrc(a.C);
   int par = 0;
   int since_flush = 0;  // centers since the private rows were written back
+  unsigned dirty = 0, flushes = 0, hits_l = 0;  // private rows: this wave's dirty mask and flush statistics
   if (a.priv_n > 0) {
     for (int k = threadIdx.x; k < kSnPriv<KB, NW> * NW * KB * kSnTile; k += blockDim.x) (&sh.priv[0][0])[k] = 0.f;
     __syncthreads();
@@ -432,9 +490,9 @@ __global__ __launch_bounds__(NW * kWave, WAVES_PER_SIMD) void train_shared_neg_k
         wave_lds_order();
       }
       for (int b = 0; b < n_batch; ++b) {
-        sn_center<KB, NW>(a, sh, rW, rC, wave, lane, t_done + b, nk, b, alpha, par, cnt, prof);
+        sn_center<KB, NW>(a, sh, rW, rC, wave, lane, t_done + b, nk, b, alpha, par, cnt, prof, dirty);
         if (a.priv_n > 0 && ++since_flush >= a.flush_every) {
-          sn_flush_private<KB, NW>(a, sh, rC, wave, lane);
+          sn_flush_private<KB, NW>(a, sh, wave, lane, dirty, flushes, hits_l);
           since_flush = 0;
         }
       }
@@ -443,7 +501,7 @@ __global__ __launch_bounds__(NW * kWave, WAVES_PER_SIMD) void train_shared_neg_k
     if (threadIdx.x == 0) atomicAdd(a.words, (unsigned long long)len);
     cnt.sentences += 1;
   }
-  if (a.priv_n > 0) sn_flush_private<KB, NW>(a, sh, rC, wave, lane);
+  if (a.priv_n > 0) sn_flush_private<KB, NW>(a, sh, wave, lane, dirty, flushes, hits_l);
 #ifdef W2V_SN_PROF
   prof.stamp(0);
   if (lane == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))
