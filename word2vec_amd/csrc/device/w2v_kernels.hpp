@@ -51,6 +51,10 @@ constexpr int kWave = 64;
 // holds; wider rows keep 4-wave workgroups.
 template <int NV>
 constexpr int kMaxBlock = NV <= 6 ? 1024 : 256;
+// Waves per SIMD the epoch kernel is compiled for: two 16-wave workgroups per
+// CU when a row is <= 2 floats per lane (d <= 128: 64 VGPRs), else one.
+template <int NV>
+constexpr int kMinWaves = NV <= 2 ? 8 : 4;
 
 struct TrainArgs {
   float* W;
@@ -640,7 +644,7 @@ __device__ __forceinline__ void center(const TrainArgs& a, float* lds, const int
 // The epoch kernel: wavefronts dequeue sentences (Word2Vec.cpp:375-394).
 // ---------------------------------------------------------------------------
 template <int NV, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY>
-__global__ __launch_bounds__(kMaxBlock<NV>) void train_epoch_kernel(TrainArgs a) {
+__global__ __launch_bounds__(kMaxBlock<NV>, kMinWaves<NV>) void train_epoch_kernel(TrainArgs a) {
   extern __shared__ float w2v_lds[];
   const int lane = lane_id();
   float* lds = (a.priv_n + a.ctx_n) > 0 ? w2v_lds : nullptr;
