@@ -354,6 +354,7 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<KB, NW>& 
     }
     wave_lds_order();
   }
+  pf_.stamp(7);
   pf_.stamp(6);
 }
 
@@ -505,9 +506,9 @@ __global__ __launch_bounds__(NW * kWave, WAVES_PER_SIMD) void train_shared_neg_k
 #ifdef W2V_SN_PROF
   prof.stamp(0);
   if (lane == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))
-    printf("SNPROF block %u wave %d centers %llu sent %llu: %llu %llu %llu %llu %llu %llu %llu\n", blockIdx.x, wave,
-           cnt.centers, cnt.sentences, prof.acc[0], prof.acc[1], prof.acc[2], prof.acc[3], prof.acc[4], prof.acc[5],
-           prof.acc[6]);
+    printf("SNPROF block %u wave %d centers %llu sent %llu: %llu %llu %llu %llu %llu %llu %llu %llu\n", blockIdx.x,
+           wave, cnt.centers, cnt.sentences, prof.acc[0], prof.acc[1], prof.acc[2], prof.acc[3], prof.acc[4],
+           prof.acc[5], prof.acc[6], prof.acc[7]);
 #endif
   if (threadIdx.x == 0) {  // every wave counted the same centers; wave 0 reports
     atomicAdd(&a.stats[0], cnt.centers);
