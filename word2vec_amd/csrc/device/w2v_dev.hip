@@ -540,6 +540,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   // under a wave cap, narrower workgroups so the capped grid still spans the CUs.
   const int max_wpb = (h->nv <= 6 ? 1024 : 256) / w2v::kWave;
   int wpb = max_wpb;
+  if (const char* e = std::getenv("W2V_DEBUG_WPB")) wpb = std::max(1, std::min(max_wpb, std::atoi(e)));  // experiments
   if (h->max_waves > 0) {
     int64_t per = h->max_waves / (h->n_cu > 0 ? h->n_cu : 1);
     wpb = 1;
@@ -565,7 +566,9 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   a.ctx_flush_every = h->context_flush > 0 ? h->context_flush : (h->cfg.hs ? 32 : 256);
   if (h->sched == W2V_SCHED_PARALLEL) {  // the reference-exact schedule keeps per-update rounding
     const int64_t row_bytes = (int64_t)h->nv * w2v::kWave * (int64_t)sizeof(float);
-    const int64_t budget = std::min<int64_t>(160 * 1024, 10 * 1024 * (int64_t)wpb) - 4 * 136;
+    int64_t per_wave = 10 * 1024;
+    if (const char* e = std::getenv("W2V_DEBUG_LDS_PER_WAVE")) per_wave = std::atoll(e);  // experiments
+    const int64_t budget = std::min<int64_t>(160 * 1024, per_wave * (int64_t)wpb) - 4 * 136;
     int64_t fit = budget / row_bytes;
     int64_t P = std::min<int64_t>(fit, 64);
     if (h->private_rows >= 0) P = std::min<int64_t>(P, h->private_rows);
