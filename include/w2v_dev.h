@@ -175,7 +175,7 @@ int w2v_dev_reset_stats(w2v_dev* h);
  * sequential schedule (W2V_SCHED_SEQUENTIAL), which is reference-exact. */
 int w2v_dev_set_hot_rows(w2v_dev* h, int64_t hot_rows);
 int w2v_dev_set_private_rows(w2v_dev* h, int32_t n);
-/* flush_centers: workgroup centers between flushes (0 = auto: 256 for NS, 64
+/* flush_centers: workgroup centers between flushes (0 = auto: 1024 for NS, 64
  * for HS); average_over: the concurrency a private row's summed deltas are
  * scaled down to (default 8; 0 = plain sum). */
 int w2v_dev_set_private_sync(w2v_dev* h, int32_t flush_centers, float average_over);

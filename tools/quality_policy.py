@@ -29,12 +29,14 @@ CBOW_POLICIES = [("context rows off", dict(context_rows=0)), ("context flush 16"
                  ("context avg 1", dict(private_average=1.0)), ("context flush 32", dict(context_flush=32))]
 HS_POLICIES = [("flush 32", dict(flush_centers=32)), ("flush 64", dict(flush_centers=64)),
                ("flush 128", dict(flush_centers=128))]
+NS_POLICIES = [("flush 512", dict(flush_centers=512)), ("flush 1024", dict(flush_centers=1024)),
+               ("flush 4096", dict(flush_centers=4096))]
 ONLY = [p for p in sys.argv[1:] if p.startswith("policy=")]
 
 for mode in [a for a in sys.argv[1:] if a in MODES] or list(MODES):
     m = MODES[mode]
     ref = np.array([[r["analogy"], r["similarity"]] for r in GOLD["scores"][mode]]).mean(0)
-    pols = POLICIES + (CBOW_POLICIES if mode.startswith("cbow") else []) + (HS_POLICIES if mode.endswith("hs") else [])
+    pols = POLICIES + (CBOW_POLICIES if mode.startswith("cbow") else []) + (HS_POLICIES if mode.endswith("hs") else NS_POLICIES)
     if ONLY:
         pols = [p for p in pols if f"policy={p[0]}" in ONLY]
     for name, pol in pols:

@@ -547,13 +547,14 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     while (wpb * 2 <= max_wpb && wpb * 2 <= per) wpb *= 2;
   }
   // Flush interval of the privatised rows, in centers of the workgroup (about
-  // 16 centers per wave for NS, 4 per wave for HS whose top nodes every
+  // 64 centers per wave for NS, 4 per wave for HS whose top nodes every
   // update touches), and the averaging of their deltas (flush_private). A
   // flush stalls the flushing wave (its later loads wait for its atomics,
-  // vmcnt is in order) behind every other workgroup's atomics on the same top
-  // nodes: CBOW-HS runs 105 / 122 / 141 M words/s at 16 / 32 / 64, with the
-  // same planted and text8-like scores (profiles/r01_hs_flush.log).
-  a.flush_every = h->flush_centers > 0 ? h->flush_centers : (h->cfg.hs ? 64 : 256);
+  // vmcnt is in order) behind every other workgroup's atomics on the same
+  // rows: CBOW-HS runs 105 / 122 / 141 M words/s at 16 / 32 / 64, SG-NS d300
+  // 78 / 90 / 96 M at 64 / 256 / 1024, with the gates passing throughout
+  // (profiles/r01_hs_flush.log, profiles/r01_ns_flush.log).
+  a.flush_every = h->flush_centers > 0 ? h->flush_centers : (h->cfg.hs ? 64 : 1024);
   a.priv_avg = h->private_average;
   // LDS privatisation of the output layer's hottest rows (the NS target matrix
   // — C for skip-gram, W for CBOW — or the top of the Huffman tree for HS)
