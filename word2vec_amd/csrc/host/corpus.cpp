@@ -28,7 +28,16 @@
 namespace w2v_corpus {
 namespace {
 
-inline bool is_space(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\v' || c == '\f' || c == '\r'; }
+struct SpaceTable {  // the C-locale isspace set, as a byte lookup
+  bool t[256];
+  SpaceTable() {
+    for (int i = 0; i < 256; ++i) t[i] = false;
+    const char* sp = " \t\n\v\f\r";
+    for (const char* c = sp; *c; ++c) t[(unsigned char)*c] = true;
+  }
+};
+const SpaceTable kSpace;
+inline bool is_space(char c) { return kSpace.t[(unsigned char)c]; }
 
 inline uint64_t hash_bytes(const char* p, size_t n) {  // FNV-1a, 64-bit
   uint64_t h = 1469598103934665603ull;
@@ -37,13 +46,18 @@ inline uint64_t hash_bytes(const char* p, size_t n) {  // FNV-1a, 64-bit
 }
 
 // Open-addressing table of words that live in the mapped file (no copies).
+// A slot keeps the word's first 16 bytes, so matching a word of <= 16 bytes
+// (nearly all of them) touches the slot only, not its first occurrence in the
+// file (a random access into a file far larger than the caches).
 struct WordTable {
+  static const uint32_t kHead = 16;
   struct Slot {
     uint64_t hash = 0;
+    char head[kHead];
     size_t off = 0;     // first occurrence (byte offset in the file)
     uint32_t len = 0;   // 0 = empty slot
-    int64_t count = 0;
     int32_t id = -1;
+    int64_t count = 0;
   };
   std::vector<Slot> slots;
   size_t used = 0;
@@ -61,12 +75,19 @@ struct WordTable {
         s.hash = h;
         s.off = (size_t)(p - base);
         s.len = n;
+        std::memcpy(s.head, p, n < kHead ? n : kHead);
         ++used;
         return &s;
       }
-      if (s.hash == h && s.len == n && std::memcmp(base + s.off, p, n) == 0) return &s;
+      if (s.hash == h && s.len == n && same(s, p, n)) return &s;
       i = (i + 1) & m;
     }
+  }
+
+  bool same(const Slot& s, const char* p, uint32_t n) const {
+    const uint32_t k = n < kHead ? n : kHead;
+    if (std::memcmp(s.head, p, k) != 0) return false;
+    return n <= kHead || std::memcmp(base + s.off + kHead, p + kHead, n - kHead) == 0;
   }
 
   void grow() {
