@@ -56,7 +56,7 @@ typedef struct w2v_dev w2v_dev; /* opaque handle */
  * (Word2Vec.h:64-66; members Word2Vec.h:32-46). */
 typedef struct w2v_dev_config {
   int32_t word_dim;  /* Word2Vec::word_dim  (Word2Vec.h:36)                      */
-  int32_t window;    /* Word2Vec::window    (Word2Vec.h:33)                      */
+  int32_t window;    /* Word2Vec::window    (Word2Vec.h:33), 0..127              */
   int32_t negative;  /* Word2Vec::negative  (Word2Vec.h:37), 0 disables NS       */
   int32_t hs;        /* train_method == "hs" (Word2Vec.cpp:162,206,342,304)       */
   int32_t cbow;      /* model == "cbow"     (Word2Vec.cpp:387-390)               */

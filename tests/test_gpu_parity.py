@@ -116,3 +116,48 @@ def test_parallel_runs_and_counts(mode):
     exp_kept = p.sum()
     sd = np.sqrt((p * (1 - p)).sum()) + 1
     assert abs(st["centers"] - exp_kept) < 6 * sd + (0 if mode.startswith("sg") else 0.01 * exp_kept)
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("window", [40, 127])
+def test_replay_wide_window(mode, window):
+    """Windows wider than a wavefront (2 * window + 1 > 64): skip-gram loads
+    the contexts past the first 64 positions one by one, CBOW runs the
+    wide-window kernel (the span's positions held 4 per lane)."""
+    sents = zipf_sentences(6, 300, 150, seed=21, ragged=True)
+    got, want, init = _run_replay(mode, sents, dim=64, window=window, iters=1, table_size=10_000)
+    for g, w, i in zip(got, want, init):
+        if w is None:
+            continue
+        assert rel_err(g - i, w - i) < 1e-4, (mode, window)
+
+
+@pytest.mark.parametrize("mode", ["sg_ns", "cbow_ns", "cbow_hs"])
+def test_philox_sequential_wide_window(mode):
+    sents = zipf_sentences(6, 300, 150, seed=23, ragged=True)
+    dim, window, iters, ts = 64, 60, 1, 100_000
+    o = oracle_run(sents, mode, dim=dim, window=window, iters=iters, table_size=ts, train=False)
+    o.build_sample()
+    cfg = device_config(o, mode, dim, window, iters, ts, True, 0.05, 2.5e-6)
+    d = device_from_oracle(o, cfg, initial=False)
+    init = [o.matrix(k) for k in range(3)]
+    key = 0x0BAD_F00D_1234_5678
+    n = o.samples()[1].size - 1
+    order = np.random.default_rng(1).permutation(n)
+    o.train_philox(0, 1, order, key, 0)
+    d.set_rng(N.W2V_RNG_PHILOX, key)
+    d.set_schedule(N.W2V_SCHED_SEQUENTIAL)
+    d.set_progress(0)
+    st = d.train_epoch(0, order)
+    assert st["words"] == o.current_words
+    for k, g in enumerate(d.download_model()):
+        if g is not None:
+            assert rel_err(g - init[k], o.matrix(k) - init[k]) < 1e-4, (mode, k)
+
+
+def test_window_limit():
+    from word2vec_amd.device import Config, DeviceTrainer
+
+    DeviceTrainer(Config(word_dim=16, window=127, negative=5, cbow=True, table_size=1000))
+    with pytest.raises(N.DevError, match="window"):
+        DeviceTrainer(Config(word_dim=16, window=128, negative=5, table_size=1000))

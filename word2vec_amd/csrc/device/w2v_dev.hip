@@ -113,16 +113,17 @@ using KernelFn = w2v::KernelFn;
 KernelFn kernel_for(const w2v_dev* h) {
   const bool cb = h->cfg.cbow != 0, hs = h->cfg.hs != 0, ns = h->cfg.negative > 0;
   const bool rp = h->rng == W2V_RNG_REPLAY;
+  const bool wd = 2 * h->cfg.window + 1 > w2v::kWave;  // CBOW's lane-per-position context set no longer fits
   switch (h->nv) {
-    case 1: return w2v::pick_train_nv1(cb, hs, ns, rp);
-    case 2: return w2v::pick_train_nv2(cb, hs, ns, rp);
-    case 3: return w2v::pick_train_nv3(cb, hs, ns, rp);
-    case 4: return w2v::pick_train_nv4(cb, hs, ns, rp);
-    case 5: return w2v::pick_train_nv5(cb, hs, ns, rp);
-    case 6: return w2v::pick_train_nv6(cb, hs, ns, rp);
-    case 8: return w2v::pick_train_nv8(cb, hs, ns, rp);
-    case 12: return w2v::pick_train_nv12(cb, hs, ns, rp);
-    default: return w2v::pick_train_nv16(cb, hs, ns, rp);
+    case 1: return w2v::pick_train_nv1(cb, hs, ns, rp, wd);
+    case 2: return w2v::pick_train_nv2(cb, hs, ns, rp, wd);
+    case 3: return w2v::pick_train_nv3(cb, hs, ns, rp, wd);
+    case 4: return w2v::pick_train_nv4(cb, hs, ns, rp, wd);
+    case 5: return w2v::pick_train_nv5(cb, hs, ns, rp, wd);
+    case 6: return w2v::pick_train_nv6(cb, hs, ns, rp, wd);
+    case 8: return w2v::pick_train_nv8(cb, hs, ns, rp, wd);
+    case 12: return w2v::pick_train_nv12(cb, hs, ns, rp, wd);
+    default: return w2v::pick_train_nv16(cb, hs, ns, rp, wd);
   }
 }
 
@@ -166,8 +167,8 @@ int w2v_dev_create(const w2v_dev_config* cfg, w2v_dev** out) {
   *out = nullptr;
   if (cfg->word_dim <= 0) return fail(W2V_ERR_ARG, "word_dim must be > 0");
   if (cfg->word_dim > 1024) return fail(W2V_ERR_UNSUPPORTED, "word_dim > 1024 unsupported");
-  if (cfg->window < 0 || cfg->window > 31)
-    return fail(W2V_ERR_UNSUPPORTED, "window must be in [0, 31] (2*window+1 <= 64 lanes)");
+  if (cfg->window < 0 || cfg->window > w2v::kMaxWindow)
+    return fail(W2V_ERR_UNSUPPORTED, "window must be in [0, 127]");
   if (cfg->negative < 0 || cfg->negative > 63)
     return fail(W2V_ERR_UNSUPPORTED, "negative must be in [0, 63]");
   if (!cfg->hs && cfg->negative == 0)

@@ -14,17 +14,20 @@ namespace w2v {
 
 constexpr int kMaxT = 8;
 
-KernelFn W2V_CAT(pick_train_nv, W2V_NV)(bool cbow, bool hs, bool ns, bool replay) {
-#define W2V_K(CB, H, N, R) &train_epoch_kernel<W2V_NV, kMaxT, CB, H, N, R>
-#define W2V_KR(CB, H, N) (replay ? W2V_K(CB, H, N, true) : W2V_K(CB, H, N, false))
+// wide: CBOW with 2 * window + 1 > 64 (skip-gram takes any window in one kernel)
+KernelFn W2V_CAT(pick_train_nv, W2V_NV)(bool cbow, bool hs, bool ns, bool replay, bool wide) {
+#define W2V_K(CB, H, N, R, WD) &train_epoch_kernel<W2V_NV, kMaxT, CB, H, N, R, WD>
+#define W2V_KR(CB, H, N, WD) (replay ? W2V_K(CB, H, N, true, WD) : W2V_K(CB, H, N, false, WD))
+#define W2V_KW(H, N) (wide ? W2V_KR(true, H, N, true) : W2V_KR(true, H, N, false))
   if (cbow) {
-    if (hs && ns) return W2V_KR(true, true, true);
-    if (hs) return W2V_KR(true, true, false);
-    return W2V_KR(true, false, true);
+    if (hs && ns) return W2V_KW(true, true);
+    if (hs) return W2V_KW(true, false);
+    return W2V_KW(false, true);
   }
-  if (hs && ns) return W2V_KR(false, true, true);
-  if (hs) return W2V_KR(false, true, false);
-  return W2V_KR(false, false, true);
+  if (hs && ns) return W2V_KR(false, true, true, false);
+  if (hs) return W2V_KR(false, true, false, false);
+  return W2V_KR(false, false, true, false);
+#undef W2V_KW
 #undef W2V_KR
 #undef W2V_K
 }

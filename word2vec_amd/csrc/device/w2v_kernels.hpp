@@ -513,7 +513,7 @@ __device__ __forceinline__ void sg_center(const TrainArgs& a, float* lds, const 
   int slot = 0;
   for (int j = lo; j < hi; ++j) {
     if (j == i) continue;
-    const int w = readlane_i(ctx_l, j - lo);
+    const int w = (j - lo < kWave) ? readlane_i(ctx_l, j - lo) : uniform_i(sent[j]);  // window > 31: span > 64
     if (HS) hs_word<NV, MAXT>(a, w, lane, x, g, alpha, cnt, lds);
     if (NS) {
       const int gs = slot % G;
@@ -530,8 +530,61 @@ __device__ __forceinline__ void sg_center(const TrainArgs& a, float* lds, const 
 }
 
 // ---------------------------------------------------------------------------
-// CBOW center (Word2Vec.cpp:286-315).
+// CBOW center (Word2Vec.cpp:286-315): the unique context ids in ascending
+// order (std::set), then cbow_tail. row_of(r) is the r-th of them.
 // ---------------------------------------------------------------------------
+template <int NV, int MAXT, bool HS, bool NS, bool REPLAY, class RowOf>
+__device__ __forceinline__ void cbow_tail(const TrainArgs& a, float* lds, int i, int c, int n, int U, RowOf row_of,
+                                         uint32_t s, float alpha, const uint32_t*& rp, Counters& cnt, int lane) {
+  cnt.centers += 1;
+  cnt.contexts += (unsigned long long)U;
+  float h[NV], g[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) h[v] = g[v] = 0.f;
+  const PrivRows cx = ctx_rows<NV>(a, lds);  // the hottest context rows: global value + pending delta
+  if (a.strict) drain_vmem();
+  for (int r0 = 0; r0 < U; r0 += MAXT) {
+    float rr[MAXT][NV];
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t)
+      if (r0 + t < U) {
+        const int row = row_of(r0 + t);
+        load_row<NV>(a.C, row, a.pitch, a.dim, lane, row < a.hot_wc || cx.has(row), rr[t]);
+      }
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t)
+      if (r0 + t < U) {
+        const int row = row_of(r0 + t);
+        if (cx.has(row)) priv_read<NV>(cx, row, lane, rr[t]);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) h[v] += rr[t][v];
+      }
+  }
+  const float nf = (float)n;
+  if (a.cbow_mean) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) h[v] /= nf;
+  }
+  if (HS) hs_word<NV, MAXT>(a, c, lane, h, g, alpha, cnt, lds);
+  if (NS) {
+    const int nd = a.negative;
+    const int negw_l = draw_negatives<REPLAY>(a, s, (uint32_t)i, 0, nd, lane, rp);
+    cnt.draws += (unsigned long long)nd;
+    ns_word<NV, MAXT>(a, a.W, c, negw_l, 0, lane, h, g, alpha, cnt, lds);
+  }
+  if (a.cbow_mean) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) g[v] /= nf;
+  }
+  for (int r = 0; r < U; ++r) {  // C.row(id) += neu1_grad for every unique id (:315)
+    const int row = row_of(r);
+    if (cx.has(row))
+      priv_add<NV>(cx, row, a.dim, lane, g);
+    else
+      add_to_row<NV>(a.C, row, row < a.hot_wc, a.pitch, a.dim, lane, g);
+  }
+}
+
 template <int NV, int MAXT, bool HS, bool NS, bool REPLAY>
 __device__ __forceinline__ void cbow_center(const TrainArgs& a, float* lds, const int32_t* sent, int len, int i, int c, int rw,
                                             uint32_t s, float alpha, const uint32_t*& rp, Counters& cnt, int lane) {
@@ -569,60 +622,94 @@ __device__ __forceinline__ void cbow_center(const TrainArgs& a, float* lds, cons
       if (lane == rk) sid = v;
     }
   }
-  cnt.centers += 1;
-  cnt.contexts += (unsigned long long)U;
-  float h[NV], g[NV];
-#pragma unroll
-  for (int v = 0; v < NV; ++v) h[v] = g[v] = 0.f;
-  const PrivRows cx = ctx_rows<NV>(a, lds);  // the hottest context rows: global value + pending delta
-  if (a.strict) drain_vmem();
-  for (int r0 = 0; r0 < U; r0 += MAXT) {
-    float rr[MAXT][NV];
-#pragma unroll
-    for (int t = 0; t < MAXT; ++t)
-      if (r0 + t < U) {
-        const int row = readlane_i(sid, r0 + t);
-        load_row<NV>(a.C, row, a.pitch, a.dim, lane, row < a.hot_wc || cx.has(row), rr[t]);
-      }
-#pragma unroll
-    for (int t = 0; t < MAXT; ++t)
-      if (r0 + t < U) {
-        const int row = readlane_i(sid, r0 + t);
-        if (cx.has(row)) priv_read<NV>(cx, row, lane, rr[t]);
-#pragma unroll
-        for (int v = 0; v < NV; ++v) h[v] += rr[t][v];
-      }
-  }
-  const float nf = (float)n;
-  if (a.cbow_mean) {
-#pragma unroll
-    for (int v = 0; v < NV; ++v) h[v] /= nf;
-  }
-  if (HS) hs_word<NV, MAXT>(a, c, lane, h, g, alpha, cnt, lds);
-  if (NS) {
-    const int nd = a.negative;
-    const int negw_l = draw_negatives<REPLAY>(a, s, (uint32_t)i, 0, nd, lane, rp);
-    cnt.draws += (unsigned long long)nd;
-    ns_word<NV, MAXT>(a, a.W, c, negw_l, 0, lane, h, g, alpha, cnt, lds);
-  }
-  if (a.cbow_mean) {
-#pragma unroll
-    for (int v = 0; v < NV; ++v) g[v] /= nf;
-  }
-  for (int r = 0; r < U; ++r) {  // C.row(id) += neu1_grad for every unique id (:315)
-    const int row = readlane_i(sid, r);
-    if (cx.has(row))
-      priv_add<NV>(cx, row, a.dim, lane, g);
-    else
-      add_to_row<NV>(a.C, row, row < a.hot_wc, a.pitch, a.dim, lane, g);
-  }
+  cbow_tail<NV, MAXT, HS, NS, REPLAY>(a, lds, i, c, n, U, [&](int r) { return readlane_i(sid, r); }, s, alpha, rp,
+                                      cnt, lane);
 }
 
-template <int NV, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY>
+// Lane-register arrays of NCH x 64 positions: element j is lane j % 64 of register j / 64.
+template <int NCH>
+__device__ __forceinline__ int pick_lane(const int (&v)[NCH], int j) {
+  int r = 0;
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch)
+    if (ch == (j >> 6)) r = readlane_i(v[ch], j & (kWave - 1));
+  return r;
+}
+
+// CBOW center for windows wider than a wave (2 * window + 1 > 64, window <=
+// 32 * NCH - 1): the same set semantics and visiting order as cbow_center, the
+// span's positions held NCH per lane (position lo + 64 ch + lane).
+template <int NV, int MAXT, bool HS, bool NS, bool REPLAY, int NCH>
+__device__ __forceinline__ void cbow_center_wide(const TrainArgs& a, float* lds, const int32_t* sent, int len, int i,
+                                                 int c, int rw, uint32_t s, float alpha, const uint32_t*& rp,
+                                                 Counters& cnt, int lane) {
+  const int lo = max(0, i - a.window + rw), hi = min(len, i + a.window + 1 - rw);
+  const int n = hi - lo - 1;
+  if (n <= 0) return;
+  const int span = hi - lo;
+  const int me = i - lo;
+  int id[NCH];
+  bool dup[NCH];
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int p = kWave * ch + lane;
+    const bool valid = p < span && p != me;
+    id[ch] = valid ? sent[lo + p] : 0;
+    dup[ch] = !valid;
+  }
+  for (int j = 0; j < span; ++j) {  // a later position repeating an earlier valid id is a duplicate
+    if (j == me) continue;
+    const int v = pick_lane<NCH>(id, j);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) dup[ch] = dup[ch] || (j < kWave * ch + lane && v == id[ch]);
+  }
+  unsigned long long uq[NCH];
+  int U = 0;
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    uq[ch] = ballot(!dup[ch]);
+    U += __popcll(uq[ch]);
+  }
+  int rank[NCH], sid[NCH];
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) rank[ch] = sid[ch] = 0;
+#pragma unroll
+  for (int c2 = 0; c2 < NCH; ++c2) {
+    unsigned long long m = uq[c2];
+    while (m) {
+      const int b = __builtin_ctzll(m);
+      m &= m - 1;
+      const int v = readlane_i(id[c2], b);
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) rank[ch] += (v < id[ch]) ? 1 : 0;
+    }
+  }
+#pragma unroll
+  for (int c2 = 0; c2 < NCH; ++c2) {
+    unsigned long long m = uq[c2];
+    while (m) {
+      const int b = __builtin_ctzll(m);
+      m &= m - 1;
+      const int v = readlane_i(id[c2], b), rk = readlane_i(rank[c2], b);
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch)
+        if (ch == (rk >> 6) && lane == (rk & (kWave - 1))) sid[ch] = v;
+    }
+  }
+  cbow_tail<NV, MAXT, HS, NS, REPLAY>(a, lds, i, c, n, U, [&](int r) { return pick_lane<NCH>(sid, r); }, s, alpha,
+                                      rp, cnt, lane);
+}
+
+constexpr int kWideChunks = 4;  // wide-window CBOW kernels: window <= 32 * kWideChunks - 1
+constexpr int kMaxWindow = 32 * kWideChunks - 1;
+
+template <int NV, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY, bool WIDE>
 __device__ __forceinline__ void center(const TrainArgs& a, float* lds, const int32_t* sent, int len, int i, int c,
                                        int rw, uint32_t s, float alpha, const uint32_t*& rp, Counters& cnt,
                                        int lane) {
-  if (CBOW)
+  if (CBOW && WIDE)
+    cbow_center_wide<NV, MAXT, HS, NS, REPLAY, kWideChunks>(a, lds, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
+  else if (CBOW)
     cbow_center<NV, MAXT, HS, NS, REPLAY>(a, lds, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
   else
     sg_center<NV, MAXT, HS, NS, REPLAY>(a, lds, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
@@ -643,7 +730,7 @@ __device__ __forceinline__ void center(const TrainArgs& a, float* lds, const int
 // ---------------------------------------------------------------------------
 // The epoch kernel: wavefronts dequeue sentences (Word2Vec.cpp:375-394).
 // ---------------------------------------------------------------------------
-template <int NV, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY>
+template <int NV, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY, bool WIDE>
 __global__ __launch_bounds__(kMaxBlock<NV>, kMinWaves<NV>) void train_epoch_kernel(TrainArgs a) {
   extern __shared__ float w2v_lds[];
   const int lane = lane_id();
@@ -685,7 +772,7 @@ __global__ __launch_bounds__(kMaxBlock<NV>, kMinWaves<NV>) void train_epoch_kern
         if (a.keep[c] < u) continue;
         const int rw = (int)rp[0];
         ++rp;
-        center<NV, MAXT, CBOW, HS, NS, REPLAY>(a, lds, sent, len, i, c, rw, (uint32_t)s, alpha, rp, cnt, lane);
+        center<NV, MAXT, CBOW, HS, NS, REPLAY, WIDE>(a, lds, sent, len, i, c, rw, (uint32_t)s, alpha, rp, cnt, lane);
       }
     } else {
       for (int i0 = 0; i0 < len; i0 += kWave) {
@@ -702,8 +789,8 @@ __global__ __launch_bounds__(kMaxBlock<NV>, kMinWaves<NV>) void train_epoch_kern
           const int b = __builtin_ctzll(kept);
           kept &= kept - 1;
           const int c = readlane_i(c_l, b), rw = readlane_i(rw_l, b);
-          center<NV, MAXT, CBOW, HS, NS, REPLAY>(a, lds, sent, len, i0 + b, c, rw, (uint32_t)s, alpha, rp, cnt,
-                                                  lane);
+          center<NV, MAXT, CBOW, HS, NS, REPLAY, WIDE>(a, lds, sent, len, i0 + b, c, rw, (uint32_t)s, alpha, rp,
+                                                        cnt, lane);
         }
       }
     }

@@ -9,7 +9,7 @@ using KernelFn = void (*)(TrainArgs);
 using ApplyFn = void (*)(float*, int64_t, int, const float*, float*, const uint8_t*, int, float, int);
 
 #define W2V_DECLARE_NV(N)                                            \
-  KernelFn pick_train_nv##N(bool cbow, bool hs, bool ns, bool replay); \
+  KernelFn pick_train_nv##N(bool cbow, bool hs, bool ns, bool replay, bool wide); \
   ApplyFn pick_apply_nv##N();
 W2V_DECLARE_NV(1)
 W2V_DECLARE_NV(2)
