@@ -561,7 +561,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   // — C for skip-gram, W for CBOW — or the top of the Huffman tree for HS)
   // and, for CBOW, of the hottest context rows of C (contexts are not
   // subsampled: the most frequent words sit in most windows): as many rows as
-  // fit 10 KiB per wave of the workgroup, <= 64 per range (the dirty masks),
+  // fit 10 KiB per wave of the workgroup, <= kPrivMax per range (the dirty masks),
   // the output rows first. Layout: lds_header_words in w2v_kernels.hpp.
   size_t lds_bytes = 0;
   a.priv_M = nullptr;
@@ -574,9 +574,13 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     const int64_t row_bytes = (int64_t)h->nv * w2v::kWave * (int64_t)sizeof(float);
     int64_t per_wave = 10 * 1024;
     if (const char* e = std::getenv("W2V_DEBUG_LDS_PER_WAVE")) per_wave = std::atoll(e);  // experiments
-    const int64_t budget = std::min<int64_t>(160 * 1024, per_wave * (int64_t)wpb) - 4 * 136;
+    const int64_t budget =
+        std::min<int64_t>(160 * 1024, per_wave * (int64_t)wpb) - 4 * w2v::lds_header_words(w2v::kPrivMax, 64);
     int64_t fit = budget / row_bytes;
-    int64_t P = std::min<int64_t>(fit, 64);
+    // <= 64 output rows by default: 128 (kPrivMax) cost 12 points of
+    // text8-like similarity on SG-NS (the averaged flush under-trains the
+    // less contended rows 64..127); an explicit private_rows may ask for more
+    int64_t P = std::min<int64_t>(fit, h->private_rows > 0 ? w2v::kPrivMax : 64);
     if (h->private_rows >= 0) P = std::min<int64_t>(P, h->private_rows);
     const bool hs = h->cfg.hs != 0;
     const int64_t avail = hs ? h->V - 1 : h->V;

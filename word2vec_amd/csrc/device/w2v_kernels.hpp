@@ -172,14 +172,16 @@ __device__ __forceinline__ uint32_t philox_table_pos(const TrainArgs& a, uint32_
 
 // ---------------------------------------------------------------------------
 // LDS-privatised rows of the per-pair kernel (when priv_n + ctx_n > 0), per workgroup:
-//   words [0,1] dirty mask of the output rows, [2,3] of the context rows,
-//   [4] centers of the workgroup, [5] / [6] flushes of either range, [7] unused,
-//   [8, 8 + priv_n) and [8 + priv_n, 8 + priv_n + ctx_n) per-row flush hits,
-//   then (from lds_header_words) the pending deltas: priv_n output rows, then
-//   ctx_n context rows, NV * 64 floats each.
+//   words [0,4) dirty mask of the output rows (2 x 64 bits), [4,8) of the
+//   context rows, [8] centers of the workgroup, [9] / [10] flushes of either
+//   range, [11] unused, [12, 12 + priv_n) and [12 + priv_n, 12 + priv_n +
+//   ctx_n) per-row flush hits, then (from lds_header_words) the pending
+//   deltas: priv_n output rows, then ctx_n context rows, NV * 64 floats each.
+//   Each range holds at most kPrivMax rows.
 // ---------------------------------------------------------------------------
+constexpr int kPrivMax = 128;
 __host__ __device__ inline int64_t lds_header_words(int64_t priv_n, int64_t ctx_n) {
-  return (8 + priv_n + ctx_n + 3) & ~int64_t(3);
+  return (12 + priv_n + ctx_n + 3) & ~int64_t(3);
 }
 
 struct PrivRows {  // one privatised row range [lo, lo + n) of matrix M (n == 0: none)
@@ -199,8 +201,8 @@ __device__ __forceinline__ PrivRows out_rows(const TrainArgs& a, float* lds) {
   if (lds == nullptr || a.priv_n == 0) return p;
   unsigned* u = reinterpret_cast<unsigned*>(lds);
   p.dirty = reinterpret_cast<unsigned long long*>(lds);
-  p.flushes = u + 5;
-  p.hits = u + 8;
+  p.flushes = u + 9;
+  p.hits = u + 12;
   p.delta = lds + lds_header_words(a.priv_n, a.ctx_n);
   p.M = const_cast<float*>(a.priv_M);
   p.lo = a.priv_lo;
@@ -213,9 +215,9 @@ __device__ __forceinline__ PrivRows ctx_rows(const TrainArgs& a, float* lds) {
   PrivRows p;
   if (lds == nullptr || a.ctx_n == 0) return p;
   unsigned* u = reinterpret_cast<unsigned*>(lds);
-  p.dirty = reinterpret_cast<unsigned long long*>(lds + 2);
-  p.flushes = u + 6;
-  p.hits = u + 8 + a.priv_n;
+  p.dirty = reinterpret_cast<unsigned long long*>(lds + 4);
+  p.flushes = u + 10;
+  p.hits = u + 12 + a.priv_n;
   p.delta = lds + lds_header_words(a.priv_n, a.ctx_n) + (int64_t)a.priv_n * (NV * kWave);
   p.M = const_cast<float*>(a.ctx_M);
   p.lo = 0;
@@ -294,7 +296,7 @@ __device__ __forceinline__ void priv_add(const PrivRows& pr, int64_t row, int d,
 #pragma unroll
   for (int v = 0; v < NV; ++v)
     if (lane + kWave * v < d) atomicAdd(q + kWave * v, delta[v]);
-  if (lane == 0) atomicOr(pr.dirty, 1ull << p);
+  if (lane == 0) atomicOr(pr.dirty + (p >> 6), 1ull << (p & 63));
 }
 
 // ---------------------------------------------------------------------------
@@ -375,11 +377,15 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
 template <int NV>
 __device__ __forceinline__ void flush_private(const TrainArgs& a, const PrivRows& pr, int lane) {
   if (pr.n == 0) return;
-  unsigned long long m = 0;
-  if (lane == 0) m = atomicExch(pr.dirty, 0ull);
-  m = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(m >> 32)) << 32) |
-      (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)m);
-  if (m == 0) return;
+  unsigned long long mw[2] = {0ull, 0ull};
+#pragma unroll
+  for (int w = 0; w < 2; ++w) {
+    unsigned long long m = 0;
+    if (lane == 0 && 64 * w < pr.n) m = atomicExch(pr.dirty + w, 0ull);
+    mw[w] = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(m >> 32)) << 32) |
+            (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)m);
+  }
+  if ((mw[0] | mw[1]) == 0) return;
   // Averaging (priv_avg = S > 0): a row that n workgroups update within one
   // flush interval receives the mean of their deltas scaled to at most S
   // concurrent contributions (local SGD on the few rows every wave updates),
@@ -390,8 +396,9 @@ __device__ __forceinline__ void flush_private(const TrainArgs& a, const PrivRows
     if (lane == 0) fl = atomicAdd(pr.flushes, 1u) + 1u;
     flushes = (float)(unsigned)__builtin_amdgcn_readfirstlane((int)fl);
   }
-  while (m) {
-    const int p = __builtin_ctzll(m);
+  for (int w = 0; w < 2; ++w)
+  for (unsigned long long m = mw[w]; m;) {
+    const int p = 64 * w + __builtin_ctzll(m);
     m &= m - 1;
     float sc = 1.0f;
     if (a.priv_avg > 0.0f) {
@@ -718,7 +725,7 @@ __device__ __forceinline__ void center(const TrainArgs& a, float* lds, const int
     // center count, and the wave that completes every flush_every-th center
     // drains the deltas all of them accumulated (one atomic per dirty row
     // instead of one per update and wave).
-    unsigned* done = reinterpret_cast<unsigned*>(lds) + 4;
+    unsigned* done = reinterpret_cast<unsigned*>(lds) + 8;
     unsigned n = 0;
     if (lane == 0) n = atomicAdd(done, 1u) + 1u;
     n = (unsigned)__builtin_amdgcn_readfirstlane((int)n);
