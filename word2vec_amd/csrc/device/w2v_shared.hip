@@ -1,6 +1,8 @@
 // Instantiations of the shared-negatives minibatch kernel (w2v_shared.hpp):
 // the row pitch decides the waves per center (2 up to 512 floats, 4 beyond)
-// and the 16-column blocks per wave; w2v_dev.hip dispatches.
+// and the 16-column blocks per wave; w2v_dev.hip dispatches. (d512 over 4
+// waves of 8 blocks, LDS-limited to 2 workgroups per CU: 62.3 vs 67.8 M
+// words/s on configs[4].)
 #include "w2v_launch.hpp"
 #include "w2v_shared.hpp"
 
