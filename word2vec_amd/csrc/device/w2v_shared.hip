@@ -10,7 +10,7 @@ namespace w2v {
 
 template <int KB, int NW>
 static KernelFn pick_occ(int) {
-  return &train_shared_neg_kernel<KB, NW, 1>;
+  return &train_shared_neg_kernel<KB, NW, 2>;
 }
 
 KernelFn pick_shared_neg(int64_t pitch, int occ, int* waves) {

@@ -145,6 +145,33 @@ __device__ __forceinline__ void store_pair(f32x4 lo, f32x4 hi, __amdgpu_buffer_r
   if (low ? ok_p : ok) store_row4(low ? hp : lo, r, low ? off_p : off, low ? coh_p : coh);
 }
 
+// Gather two consecutive 16-column blocks (block 2j, 2j+1) as two
+// instructions of 8 rows x 128 contiguous bytes (store_pair's inverse):
+// instruction 0 reads rows 0..7 — lane col < 8 its own block 2j, lane col >= 8
+// the block 2j+1 of row col - 8 (its partner col ^ 8) — instruction 1 rows
+// 8..15 the same way. The raw results land in (t0, t1); pair_fixup later puts
+// the lane's own blocks there (own block 2j from whichever instruction read
+// it, own block 2j+1 from the partner through DPP row_ror:8), after the loads
+// have been issued for every block.
+__device__ __forceinline__ void load_pair(f32x4& t0, f32x4& t1, __amdgpu_buffer_rsrc_t r, uint32_t off, bool coh,
+                                          int col) {
+  const uint32_t off_p = (uint32_t)dpp_i<0x128>((int)off) + 64u;  // partner row, block 2j+1
+  const bool coh_p = dpp_i<0x128>((int)coh) != 0;
+  const bool low = col < 8;
+  t0 = load_row4(r, low ? off : off_p, low ? coh : coh_p);
+  t1 = load_row4(r, low ? off_p : off, low ? coh_p : coh);
+}
+__device__ __forceinline__ void pair_fixup(f32x4& t0, f32x4& t1, int col) {
+  const bool low = col < 8;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float own = low ? t0[e] : t1[e];
+    const float other = low ? t1[e] : t0[e];  // the partner's block 2j+1
+    t0[e] = own;
+    t1[e] = __int_as_float(dpp_i<0x128>(__float_as_int(other)));
+  }
+}
+
 // Keep this wave's LDS accesses in program order (the LDS unit serves one
 // wave's operations in order; this only stops the compiler reordering them).
 __device__ __forceinline__ void wave_lds_order() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
@@ -205,7 +232,7 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<KB, NW>& 
   if (a.strict) drain_vmem();  // sequential schedule: this wave's own stores land before the re-read
   f32x4 wr[KB], cr[KB];
 #pragma unroll
-  for (int kb = 0; kb < KB; ++kb) wr[kb] = load_row4(rW, wo + 64u * kb, w_coh);
+  for (int kb = 0; kb < KB; kb += 2) load_pair(wr[kb], wr[kb + 1], rW, wo + 64u * kb, w_coh, col);
   // outputs: lane 0 the center, lane t in [1, K] the (t-1)-th shared draw
   const int K = a.negative;
   const int prev_draw = sh.draw[b][(lane + kSnTile - 1) & (kSnTile - 1)];
@@ -232,12 +259,17 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<KB, NW>& 
     }
   }
 #pragma unroll
-  for (int kb = 0; kb < KB; ++kb) cr[kb] = load_row4(rC, co + 64u * kb, c_coh);
+  for (int kb = 0; kb < KB; kb += 2) load_pair(cr[kb], cr[kb + 1], rC, co + 64u * kb, c_coh, col);
   cnt.centers += 1;
   cnt.contexts += (unsigned long long)M;
   cnt.targets += (unsigned long long)__popcll(okm);
   cnt.draws += (unsigned long long)K;
   pf_.stamp(1);
+#pragma unroll
+  for (int kb = 0; kb < KB; kb += 2) {
+    pair_fixup(wr[kb], wr[kb + 1], col);
+    pair_fixup(cr[kb], cr[kb + 1], col);
+  }
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
   if (c_priv) {
 #pragma unroll
