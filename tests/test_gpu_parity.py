@@ -118,6 +118,43 @@ def test_parallel_runs_and_counts(mode):
     assert abs(st["centers"] - exp_kept) < 6 * sd + (0 if mode.startswith("sg") else 0.01 * exp_kept)
 
 
+@pytest.mark.parametrize("mode", ["sg_ns", "cbow_hs", "sg_hs"])
+def test_parallel_segments_match_whole_sentences(mode, monkeypatch):
+    """Sentence segments as work items (w2v_dev.hip kSegLen): one wave taking a
+    sentence's segments in turn trains exactly what it trains taking the whole
+    sentence (same centers, windows over the whole sentence, same Philox draws,
+    same flush points); fixed alpha, since the schedule reads the word counter,
+    which segments advance earlier."""
+    sents = zipf_sentences(6, 700, 300, seed=13, ragged=True)
+    dim = 100
+    o = oracle_run(sents, mode, dim=dim, window=5, iters=1, table_size=100_000, train=False)
+    o.build_sample()
+    cfg = device_config(o, mode, dim, 5, 1, 100_000, True, 0.05, 2.5e-6)
+    ids, off = o.samples()
+    assert np.diff(off).max() > 128  # more than one segment per sentence
+    order = np.random.default_rng(1).permutation(off.size - 1)
+    out = {}
+    for seg in ("0", "64", "128"):
+        monkeypatch.setenv("W2V_SEG_LEN", seg)
+        d = device_from_oracle(o, cfg, initial=False)
+        d.set_rng(N.W2V_RNG_PHILOX, 99)
+        d.set_schedule(N.W2V_SCHED_PARALLEL)
+        d.set_max_waves(1)
+        d.set_fixed_alpha(0.025)
+        d.set_progress(0)
+        st = d.train_epoch(0, order)
+        out[seg] = (st, d.download_model())
+        d.close()
+    st0, m0 = out["0"]
+    assert st0["words"] == ids.size and st0["sentences"] == off.size - 1
+    for seg in ("64", "128"):
+        st, m = out[seg]
+        assert st == st0, seg
+        for a, b in zip(m0, m):
+            if a is not None:
+                np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("mode", list(MODES))
 @pytest.mark.parametrize("window", [40, 127])
 def test_replay_wide_window(mode, window):

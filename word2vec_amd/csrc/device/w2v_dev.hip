@@ -58,6 +58,11 @@ void dfree(T*& p) {
 
 }  // namespace
 
+// Work-item size of the parallel Philox schedule (tokens of a sentence per
+// item) and the most items a sentence is cut into.
+constexpr int64_t kSegLen = 128;
+constexpr int64_t kMaxSeg = 64;
+
 struct w2v_dev {
   w2v_dev_config cfg{};
   int device = 0;
@@ -87,6 +92,7 @@ struct w2v_dev {
   int32_t* ids = nullptr;
   int64_t* soff = nullptr;
   int64_t n_tok = 0, n_sent = 0, train_words = 0;
+  int64_t max_len = 0;        // longest sentence (tokens)
   int64_t* order = nullptr;
   uint32_t* replay = nullptr;
   int64_t* replay_off = nullptr;
@@ -410,9 +416,12 @@ int w2v_dev_upload_corpus(w2v_dev* h, const int32_t* ids, int64_t n_tok, const i
   if (n_sent < 0 || n_tok < 0 || n_sent > (int64_t)UINT32_MAX - 1)
     return fail(W2V_ERR_ARG, "corpus sizes out of range");
   if (soff[0] != 0 || soff[n_sent] != n_tok) return fail(W2V_ERR_ARG, "sentence offsets must span [0, n_tokens]");
-  for (int64_t s = 0; s < n_sent; ++s)
+  int64_t max_len = 0;
+  for (int64_t s = 0; s < n_sent; ++s) {
     if (soff[s] > soff[s + 1] || soff[s + 1] - soff[s] > (int64_t)INT32_MAX)
       return fail(W2V_ERR_ARG, "sentence offsets must be non-decreasing");
+    max_len = std::max<int64_t>(max_len, soff[s + 1] - soff[s]);
+  }
   if (h->V < 1) return fail(W2V_ERR_STATE, "upload the vocab before the corpus");
   for (int64_t t = 0; t < n_tok; ++t)
     if (ids[t] < 0 || ids[t] >= h->V) return fail(W2V_ERR_ARG, "token id out of vocab range");
@@ -426,6 +435,7 @@ int w2v_dev_upload_corpus(w2v_dev* h, const int32_t* ids, int64_t n_tok, const i
   HIP_TRY(hipMalloc(&h->order, (n_sent > 0 ? n_sent : 1) * sizeof(int64_t)));
   h->n_tok = n_tok;
   h->n_sent = n_sent;
+  h->max_len = max_len;
   h->train_words = train_words;
   h->corpus_ready = true;
   return W2V_OK;
@@ -668,6 +678,35 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     }
     grid = dim3((unsigned)g);
     block = dim3(threads);
+  }
+  // Sentence segments as work items (parallel Philox schedule): the launch's
+  // last round shrinks from a whole sentence per wave to one segment. With
+  // ~1000-token sentences and a few thousand resident waves, whole sentences
+  // leave most of the chip idle for the last ~1/rounds of the launch. Only
+  // when the sentences alone fill the grid: segments must not raise the
+  // number of waves training at once (a small corpus would train its
+  // frequent rows from more waves at once than whole sentences do; the
+  // planted CBOW-HS gate loses 3.6 points of similarity that way).
+  a.nseg = 1;
+  a.seg_len = 0;
+  if (h->sched == W2V_SCHED_PARALLEL && h->rng == W2V_RNG_PHILOX && count >= (int64_t)grid.x * block.x / w2v::kWave) {
+    int64_t seg = kSegLen;
+    if (const char* e = std::getenv("W2V_SEG_LEN")) seg = std::atoll(e);  // experiments; 0 = whole sentences
+    if (seg > 0) {
+      seg = (seg + w2v::kWave - 1) / w2v::kWave * w2v::kWave;
+      int64_t nseg = (h->max_len + seg - 1) / seg;
+      if (nseg > kMaxSeg) {  // very long sentences: longer segments, not more
+        nseg = kMaxSeg;
+        seg = ((h->max_len + nseg - 1) / nseg + w2v::kWave - 1) / w2v::kWave * w2v::kWave;
+      }
+      // the dequeue head is 32-bit: items plus one extra dequeue per wave
+      while (nseg > 1 && count * nseg > (int64_t)UINT32_MAX - (1 << 24)) --nseg;
+      if (nseg > 1) {
+        seg = ((h->max_len + nseg - 1) / nseg + w2v::kWave - 1) / w2v::kWave * w2v::kWave;
+        a.nseg = (int32_t)nseg;
+        a.seg_len = (int32_t)seg;
+      }
+    }
   }
   hipLaunchKernelGGL(fn, grid, block, lds_bytes, h->stream, a);
   HIP_TRY(hipGetLastError());

@@ -100,6 +100,8 @@ struct TrainArgs {
   int32_t ctx_flush_every;     // centers of the workgroup between flushes of the context rows
   int64_t item0;               // shared-negatives kernel: work items are order[item0 + k] (or item0 + k)
   int64_t hot_atomic;          // shared-negatives kernel: W / C rows [0, hot_atomic) take memory-side atomic deltas
+  int32_t nseg;                // work items per sentence (parallel Philox schedule; 1 = whole sentences)
+  int32_t seg_len;             // tokens per item when nseg > 1 (a multiple of 64)
 };
 
 // LDS the shared-negatives kernel gives its private C rows (w2v_shared.hpp kSnPriv; <= 32 rows).
@@ -441,15 +443,11 @@ __device__ __forceinline__ void hs_word(const TrainArgs& a, int word, int lane, 
   }
 }
 
-// NS with positive `word` against `negw_l` lanes [base, base + neg): builds the
-// target list (positive first, then first occurrences of the negatives that
-// differ from it — the set semantics of Word2Vec.cpp:253-257) and applies it.
-template <int NV, int MAXT>
-__device__ __forceinline__ void ns_word(const TrainArgs& a, float* M, int word, int negw_l, int base, int lane,
-                                        const float (&x)[NV], float (&g)[NV], float alpha, Counters& cnt,
-                                        float* lds) {
-  const PrivRows pr = (a.priv_M == M) ? out_rows<NV>(a, lds) : PrivRows();
-  const int neg = a.negative;
+// NS target list of positive `word` against `negw_l` lanes [base, base + neg):
+// lane t of tgt_l holds target t (positive first, then first occurrences of
+// the negatives that differ from it — the set semantics of
+// Word2Vec.cpp:253-257); returns the count.
+__device__ __forceinline__ int ns_targets(int neg, int word, int negw_l, int base, int lane, int& tgt_l) {
   const int nk = __shfl(negw_l, (base + lane) & (kWave - 1));
   bool dup = (lane >= neg) || (nk == word);
   for (int j = 0; j < neg - 1; ++j) {
@@ -457,7 +455,7 @@ __device__ __forceinline__ void ns_word(const TrainArgs& a, float* M, int word, 
     dup = dup || (lane > j && nk == v);
   }
   unsigned long long uniq = ballot(!dup);
-  int tgt_l = (lane == 0) ? word : 0;
+  tgt_l = (lane == 0) ? word : 0;
   int m = 1;
   while (uniq) {
     const int b = __builtin_ctzll(uniq);
@@ -466,14 +464,31 @@ __device__ __forceinline__ void ns_word(const TrainArgs& a, float* M, int word, 
     if (lane == m) tgt_l = v;
     ++m;
   }
-  const int T = m;
-  const int code_l = (lane == 0) ? 0 : 1;
+  return m;
+}
+
+// The T targets of tgt_l / code_l, MAXT rows per batch.
+template <int NV, int MAXT>
+__device__ __forceinline__ void apply_list(const TrainArgs& a, float* M, int T, int tgt_l, int code_l,
+                                           const float (&x)[NV], float (&g)[NV], float alpha, Counters& cnt,
+                                           const PrivRows& pr) {
   for (int t0 = 0; t0 < T; t0 += MAXT) {
     if (a.strict) drain_vmem();
-    apply_targets<NV, MAXT, false>(M, a.pitch, a.dim, lane, min(MAXT, T - t0), tgt_l, code_l, t0, x, g, alpha,
+    apply_targets<NV, MAXT, false>(M, a.pitch, a.dim, lane_id(), min(MAXT, T - t0), tgt_l, code_l, t0, x, g, alpha,
                                    0, a.hot_wc, pr);
   }
   cnt.targets += (unsigned long long)T;
+}
+
+// NS with positive `word` against `negw_l` lanes [base, base + neg).
+template <int NV, int MAXT>
+__device__ __forceinline__ void ns_word(const TrainArgs& a, float* M, int word, int negw_l, int base, int lane,
+                                        const float (&x)[NV], float (&g)[NV], float alpha, Counters& cnt,
+                                        float* lds) {
+  const PrivRows pr = (a.priv_M == M) ? out_rows<NV>(a, lds) : PrivRows();
+  int tgt_l;
+  const int T = ns_targets(a.negative, word, negw_l, base, lane, tgt_l);
+  apply_list<NV, MAXT>(a, M, T, tgt_l, (lane == 0) ? 0 : 1, x, g, alpha, cnt, pr);
 }
 
 // Draw table words for `ndraw` (slot, k) pairs starting at slot `slot0`:
@@ -751,11 +766,20 @@ __global__ __launch_bounds__(kMaxBlock<NV>, kMinWaves<NV>) void train_epoch_kern
   float alpha = a.init_alpha;
   bool first = true;
   const uint32_t wmax = (uint32_t)(a.window < 1 ? 1 : a.window);
+  // A work item is one sentence, or (nseg > 1: parallel Philox schedule) one
+  // seg_len-token segment of it, so that the last round of a launch is short
+  // (a few thousand waves, ~1000-token sentences: whole-sentence items leave
+  // most waves idle while the last sentences finish). Segment g of a sentence
+  // trains the centers [g * seg_len, (g + 1) * seg_len) with the whole sentence
+  // as their windows, exactly what the whole-sentence wave does for them.
+  const uint32_t nseg = (uint32_t)(a.nseg > 1 ? a.nseg : 1);
+  const int64_t n_items = a.n_sent * (int64_t)nseg;
   for (;;) {
-    uint32_t k = 0;
-    if (lane == 0) k = atomicAdd(a.work, 1u);
-    k = (uint32_t)uniform_i((int)k);
-    if ((int64_t)k >= a.n_sent) break;
+    uint32_t kk = 0;
+    if (lane == 0) kk = atomicAdd(a.work, 1u);
+    kk = (uint32_t)uniform_i((int)kk);
+    if ((int64_t)kk >= n_items) break;
+    const uint32_t k = kk / nseg, seg = kk - k * nseg;
     const int64_t s = a.order ? a.order[k] : (int64_t)k;
     if (s < 0 || s >= a.n_corpus) continue;  // a caller-supplied device order is not host-checked
     if (a.fixed_alpha > 0.0f) {
@@ -782,9 +806,11 @@ __global__ __launch_bounds__(kMaxBlock<NV>, kMinWaves<NV>) void train_epoch_kern
         center<NV, MAXT, CBOW, HS, NS, REPLAY, WIDE>(a, lds, sent, len, i, c, rw, (uint32_t)s, alpha, rp, cnt, lane);
       }
     } else {
-      for (int i0 = 0; i0 < len; i0 += kWave) {
+      const int seg_lo = nseg > 1 ? min(len, (int)seg * a.seg_len) : 0;
+      const int seg_hi = nseg > 1 ? min(len, seg_lo + a.seg_len) : len;
+      for (int i0 = seg_lo; i0 < seg_hi; i0 += kWave) {
         const int ii = i0 + lane;
-        const bool in = ii < len;
+        const bool in = ii < seg_hi;
         const int c_l = in ? sent[ii] : 0;
         const float p_l = in ? a.keep[c_l] : 0.f;
         uint32_t o0, o1, o2, o3;
@@ -801,8 +827,14 @@ __global__ __launch_bounds__(kMaxBlock<NV>, kMinWaves<NV>) void train_epoch_kern
         }
       }
     }
-    if (lane == 0) atomicAdd(a.words, (unsigned long long)len);
-    cnt.sentences += 1;
+    if (REPLAY || nseg == 1) {
+      if (lane == 0) atomicAdd(a.words, (unsigned long long)len);
+      cnt.sentences += 1;
+    } else {
+      const int seg_lo = min(len, (int)seg * a.seg_len), seg_hi = min(len, seg_lo + a.seg_len);
+      if (lane == 0 && seg_hi > seg_lo) atomicAdd(a.words, (unsigned long long)(seg_hi - seg_lo));
+      cnt.sentences += (seg == 0) ? 1 : 0;
+    }
   }
   flush_private<NV>(a, out_rows<NV>(a, lds), lane);
   flush_private<NV>(a, ctx_rows<NV>(a, lds), lane);
