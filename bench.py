@@ -376,9 +376,18 @@ def cpu_baseline(args, counts_v, ids_h, soff_h, neg, mode):
     t = time.perf_counter()
     w = o.train_omp(threads, n, 11)
     dt = time.perf_counter() - t
+    # the same loop on one thread (all host cores and 1), on a
+    # prefix sized to about a third of the budget
+    n1 = int(min(soff_h.size - 1, max(n_cal, (w / dt) / max(1, threads) * args.cpu_seconds / 3 / max(1, args.sent_len))))
+    o.set_samples(ids_h[: soff_h[n1]], soff_h[: n1 + 1], int(n1 * args.sent_len))
+    t1 = time.perf_counter()
+    w1 = o.train_omp(1, n1, 13)
+    dt1 = time.perf_counter() - t1
     return {"value": round(w / dt, 1), "unit": "words/s", "cores": threads, "kind": "port",
+            "single_thread_value": round(w1 / dt1, 1),
             "sample": f"{n} sentences ({w} in-vocab tokens) of the same shard, {dt:.1f}s, oracle OpenMP loop "
-                      f"(per-call hash map / set, static schedule, per-thread mt19937)"
+                      f"(per-call hash map / set, static schedule, per-thread mt19937); single_thread_value: "
+                      f"the same loop on 1 thread over {n1} sentences, {dt1:.1f}s"
                       + ("; the reference's per-pair update: the shared-negatives minibatch has no reference CPU path"
                          if mode.get("shared") else "")}
 
