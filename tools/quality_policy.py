@@ -20,6 +20,7 @@ from word2vec_amd.model import Word2Vec  # noqa: E402
 GOLD = json.loads((ROOT / "tests" / "golden" / "quality_oracle.json").read_text())
 SENTS, QS, PAIRS = planted_corpus(**CORPUS)
 POLICIES = [("default", {}), ("hot_rows=0", dict(hot_rows=0)), ("hot_rows=64", dict(hot_rows=64)),
+            ("hot_rows=250", dict(hot_rows=250)), ("hot_rows=500", dict(hot_rows=500)), ("hot_rows=2000", dict(hot_rows=2000)),
             ("private off", dict(private_rows=0)), ("plain Hogwild", dict(hot_rows=0, private_rows=0, context_rows=0))]
 CBOW_POLICIES = [("context rows off", dict(context_rows=0)), ("context flush 16", dict(context_flush=16)),
                  ("context flush 256", dict(context_flush=256)), ("context flush 1024", dict(context_flush=1024)),
