@@ -272,8 +272,9 @@ def main():
     bytes_per_launch = (4 * d * row_moves + 4 * delta["draws"]) / n_launch
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
     achieved = bytes_per_launch / avg_kernel_s / 1e9
+    traffic, traffic_src = pmc_traffic(args)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, bytes_per_launch),
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": "train_epoch_kernel", "avg_launch_ms": round(avg_kernel_s * 1e3, 3),
                 "algorithmic_bytes_per_launch": int(bytes_per_launch)}
     if mode.get("shared"):
@@ -328,6 +329,7 @@ def main():
                 "context_rows": args.context_rows,
                 "context_flush": args.context_flush,
                 "kept_centers_per_step": int(delta["centers"] / args.steps),
+                "env_knobs": tr.knobs(),
                 "targets_per_step": int(delta["targets"] / args.steps),
             },
             "roofline": roofline,
@@ -339,55 +341,86 @@ def main():
     tr.close()
 
 
-def pmc_traffic(args, bytes_per_launch):
-    """HBM bytes per launch from a committed rocprofv3 PMC pass of this workload, if present."""
+def pmc_traffic(args):
+    """HBM bytes per launch of this workload's dominant kernel from the committed
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh + tools/pmc_summary.py;
+    2 x FETCH + WRITE, MI355X_MICROARCH.md's gfx950 correction), with the profile
+    it came from: (bytes, source) or (None, None)."""
     f = ROOT / "profiles" / "pmc_traffic.json"
     if not f.exists():
-        return None
+        return None, None
     try:
-        rec = json.loads(f.read_text())
-        key = f"{args.mode}_d{args.dim}_n{args.tokens}"
-        return rec.get(key)
-    except Exception:
-        return None
+        rec = json.loads(f.read_text()).get(f"{args.mode}_d{args.dim}_n{args.tokens}")
+    except (OSError, ValueError):
+        return None, None
+    if isinstance(rec, dict):
+        return rec.get("traffic"), rec.get("source")
+    return None, None
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def cpu_baseline(args, counts_v, ids_h, soff_h, neg, mode):
-    """The oracle's OpenMP restatement of the reference loop on the host cores,
-    over a bounded prefix of the same shard (same params)."""
-    from oracle import Oracle
+    """The reference's OpenMP training loop (Word2Vec.cpp:375-394; restated in
+    oracle/w2v_oracle.cpp with its per-call hash map / set, static schedule,
+    shared alpha) compiled with the reference's own flags (main.cpp:2: -Ofast
+    -march=native -funroll-loops -fopenmp, built on this host), timed on the
+    host cores over a bounded prefix of the same shard (same params):
+      value                     all OMP_NUM_THREADS threads, ONE shared mt19937 (the reference's data race)
+      per_thread_rng_value      the same, one mt19937 per thread
+      single_thread_value       one thread"""
+    import oracle
 
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    o = Oracle(iter=1, window=args.window, min_count=args.min_count, table_size=args.table_size,
-               word_dim=args.dim, negative=neg, subsample_threshold=args.subsample, init_alpha=0.025,
-               min_alpha=2.5e-6, cbow_mean=True, train_method="hs" if mode["hs"] else "ns",
-               model="cbow" if mode["cbow"] else "sg")
-    o.set_vocab_counts(counts_v)
-    o.seed(args.seed)
-    # calibrate on a small prefix, then time a prefix sized to the budget
-    n_cal = 32
-    o.set_samples(ids_h[: soff_h[n_cal]], soff_h[: n_cal + 1], int(n_cal * args.sent_len))
-    o.init_weights()
-    t = time.perf_counter()
-    w = o.train_omp(threads, n_cal, 7)
-    rate = w / max(time.perf_counter() - t, 1e-6)
-    n = int(min(soff_h.size - 1, max(n_cal, rate * args.cpu_seconds / max(1, args.sent_len))))
-    o.set_samples(ids_h[: soff_h[n]], soff_h[: n + 1], int(n * args.sent_len))
-    t = time.perf_counter()
-    w = o.train_omp(threads, n, 11)
-    dt = time.perf_counter() - t
-    # the same loop on one thread (SURVEY.md §8(d): all host cores and 1), on a
-    # prefix sized to about a third of the budget
-    n1 = int(min(soff_h.size - 1, max(n_cal, (w / dt) / max(1, threads) * args.cpu_seconds / 3 / max(1, args.sent_len))))
-    o.set_samples(ids_h[: soff_h[n1]], soff_h[: n1 + 1], int(n1 * args.sent_len))
-    t1 = time.perf_counter()
-    w1 = o.train_omp(1, n1, 13)
-    dt1 = time.perf_counter() - t1
+    path, flags = oracle.build_fast()
+    native = oracle.BaselineLib(path)
+
+    def make():
+        o = oracle.Oracle(iter=1, window=args.window, min_count=args.min_count, table_size=args.table_size,
+                          word_dim=args.dim, negative=neg, subsample_threshold=args.subsample, init_alpha=0.025,
+                          min_alpha=2.5e-6, cbow_mean=True, train_method="hs" if mode["hs"] else "ns",
+                          model="cbow" if mode["cbow"] else "sg", native=native)
+        o.set_vocab_counts(counts_v)
+        o.seed(args.seed)
+        return o
+
+    def timed(o, nthreads, budget, shared, seed):
+        # calibrate on a small prefix, then time a prefix sized to the budget
+        n_cal = 32
+        o.set_samples(ids_h[: soff_h[n_cal]], soff_h[: n_cal + 1], int(n_cal * args.sent_len))
+        o.init_weights()
+        t = time.perf_counter()
+        w = o.train_omp(nthreads, n_cal, seed, shared)
+        rate = w / max(time.perf_counter() - t, 1e-6)
+        n = int(min(soff_h.size - 1, max(n_cal, rate * budget / max(1, args.sent_len))))
+        o.set_samples(ids_h[: soff_h[n]], soff_h[: n + 1], int(n * args.sent_len))
+        o.init_weights()
+        t = time.perf_counter()
+        w = o.train_omp(nthreads, n, seed + 1, shared)
+        dt = time.perf_counter() - t
+        return w, dt, n
+
+    o = make()
+    w, dt, n = timed(o, threads, args.cpu_seconds, True, 11)
+    wp, dtp, n_p = timed(o, threads, args.cpu_seconds / 2, False, 21)
+    w1, dt1, n1 = timed(o, 1, args.cpu_seconds / 3, True, 31)
     return {"value": round(w / dt, 1), "unit": "words/s", "cores": threads, "kind": "port",
+            "per_thread_rng_value": round(wp / dtp, 1),
             "single_thread_value": round(w1 / dt1, 1),
-            "sample": f"{n} sentences ({w} in-vocab tokens) of the same shard, {dt:.1f}s, oracle OpenMP loop "
-                      f"(per-call hash map / set, static schedule, per-thread mt19937); single_thread_value: "
-                      f"the same loop on 1 thread over {n1} sentences, {dt1:.1f}s"
+            "cpu": cpu_model(), "host_cpus": os.cpu_count(), "flags": flags,
+            "sample": f"{n} sentences ({w} in-vocab tokens) of the same shard, {dt:.1f}s: the reference's OpenMP "
+                      f"loop restated (oracle/w2v_oracle.cpp orc_train_omp_shared), built with {flags}, "
+                      f"{threads} threads sharing one mt19937 as the reference does; per_thread_rng_value: "
+                      f"{n_p} sentences, {dtp:.1f}s, one mt19937 per thread; single_thread_value: {n1} sentences, "
+                      f"{dt1:.1f}s"
                       + ("; the reference's per-pair update: the shared-negatives minibatch has no reference CPU path"
                          if mode.get("shared") else "")}
 

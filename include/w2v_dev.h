@@ -36,6 +36,7 @@ extern "C" {
 #define W2V_ERR_HIP 2         /* a HIP runtime call failed */
 #define W2V_ERR_STATE 3       /* call out of order (e.g. train before upload) */
 #define W2V_ERR_UNSUPPORTED 4 /* configuration outside the kernels' range */
+#define W2V_ERR_DIVERGED 5    /* training produced non-finite values (w2v_dev_stats.nonfinite) */
 
 /* RNG modes for the training kernels. */
 #define W2V_RNG_PHILOX 0 /* counter-based Philox4x32-10 per (epoch, sentence, position, slot, k) */
@@ -78,11 +79,19 @@ typedef struct w2v_dev_stats {
   int64_t targets;   /* output rows updated: NS targets + HS path nodes          */
   int64_t draws;     /* unigram-table draws (Word2Vec.cpp:255)                   */
   int64_t sentences; /* sentences processed                                      */
+  int64_t nonfinite; /* sigma arguments (row . input) that were not finite: the
+                        model diverged. w2v_dev_train_epoch returns
+                        W2V_ERR_DIVERGED when its epoch raised this count;
+                        _async callers check it with w2v_dev_read_stats          */
 } w2v_dev_stats;
 
 /* Library / error. */
 const char* w2v_dev_version(void);
 const char* w2v_dev_last_error(void); /* thread-local message of the last failure */
+/* The experiment environment variables (W2V_SEG_LEN, W2V_DEBUG_*, W2V_SN_*)
+ * this handle read at w2v_dev_create, as "NAME=value ..." ("" when none was
+ * set). They are read once there, never per launch. */
+const char* w2v_dev_knobs(w2v_dev* h);
 
 /* Replaces: the Word2Vec ctor's device-relevant state (Word2Vec.cpp:12-17). */
 int w2v_dev_create(const w2v_dev_config* cfg, w2v_dev** out);
@@ -143,6 +152,8 @@ int w2v_dev_get_progress(w2v_dev* h, int64_t* current_words);
 int w2v_dev_train_epoch(w2v_dev* h, int32_t epoch, const int64_t* order, w2v_dev_stats* stats);
 /* The same, enqueued on the handle's stream; `order_dev` is a device array or NULL. */
 int w2v_dev_train_epoch_async(w2v_dev* h, int32_t epoch, const int64_t* order_dev);
+/* (w2v_dev_train_epoch returns W2V_ERR_DIVERGED, after the epoch, when any
+ * sigma argument was non-finite; the model is then left as trained.) */
 /* Train the `count` sentences listed in the device array `order_dev` (an
  * arbitrary slice of an epoch's order), enqueued on the handle's stream: lets a
  * caller cut an epoch into rounds between model-averaging points. */

@@ -50,6 +50,8 @@ int w2v_model_file_samples(w2v_model* m, const char* path, const char* format, i
                            int64_t* n_sentences, int64_t* train_words);
 int w2v_model_copy_samples(w2v_model* m, int32_t* ids, int64_t* offsets);
 
+/* Word introspection: an index outside [0, vocab_size) returns NULL / -1 /
+ * NaN / non-zero and sets last_error. */
 int64_t w2v_model_vocab_size(w2v_model* m);
 const char* w2v_model_word(w2v_model* m, int64_t i);
 int64_t w2v_model_word_count(w2v_model* m, int64_t i);
@@ -61,7 +63,8 @@ int w2v_model_table(w2v_model* m, uint32_t* out);
 
 int64_t w2v_model_rows(w2v_model* m, int32_t which);
 int w2v_model_get_matrix(w2v_model* m, int32_t which, float* out);
-int w2v_model_set_matrix(w2v_model* m, int32_t which, const float* in, int64_t rows);
+/* in: rows x cols dense floats; cols must equal word_dim (non-zero return otherwise). */
+int w2v_model_set_matrix(w2v_model* m, int32_t which, const float* in, int64_t rows, int64_t cols);
 
 /* train_sentence_sg / train_sentence_cbow on one sentence of vocab indices. */
 int w2v_model_train_sentence(w2v_model* m, const int32_t* ids, int64_t n, float alpha, int32_t cbow);

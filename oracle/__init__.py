@@ -57,6 +57,7 @@ _SIG = {
     "orc_philox": (None, [_P, _U64, _P]),
     "orc_set_shared_negatives": (None, [_P, _I32]),
     "orc_train_omp": (_I64, [_P, _I32, _I64, _U32]),
+    "orc_train_omp_shared": (_I64, [_P, _I32, _I64, _U32, _I32]),
     "orc_set_vocab_counts": (None, [_P, _P, _I64]),
     "orc_set_samples": (None, [_P, _P, _P, _I64, _I64]),
     "orc_train_sentence": (None, [_P, _P, _I64, _F, _I32]),
@@ -67,15 +68,61 @@ _SIG = {
 _lib = None
 
 
+def _bind(path) -> C.CDLL:
+    L = C.CDLL(str(path))
+    for k, (r, a) in _SIG.items():
+        f = getattr(L, k)
+        f.restype, f.argtypes = r, a
+    return L
+
+
 def lib() -> C.CDLL:
     global _lib
     if _lib is None:
         build()
-        _lib = C.CDLL(str(LIB))
-        for k, (r, a) in _SIG.items():
-            f = getattr(_lib, k)
-            f.restype, f.argtypes = r, a
+        _lib = _bind(LIB)
     return _lib
+
+
+# The CPU-baseline build: the same restatement compiled with the reference's
+# own flags (main.cpp:2: -Ofast -march=native -funroll-loops -fopenmp). Used
+# ONLY by bench.py's cpu_baseline leg for timing — -Ofast changes the float
+# bits of the host products, so parity never uses it.
+REF_FLAGS = ["-std=c++11", "-Ofast", "-march=native", "-funroll-loops", "-fopenmp"]
+PORTABLE_FLAGS = ["-std=c++11", "-Ofast", "-march=x86-64-v3", "-funroll-loops", "-fopenmp"]
+FAST_LIB = HERE / "liboracle_fast.so"  # prebuilt with PORTABLE_FLAGS (Makefile), for boxes without g++
+
+
+def build_fast(out_dir=None):
+    """Compile the baseline build with REF_FLAGS for THIS host's CPU (-march=native
+    must be compiled where it runs). Returns (path, flags); falls back to the
+    prebuilt portable build when no compiler is available."""
+    import hashlib
+    import os
+    import shutil
+    import tempfile
+
+    src = HERE / "w2v_oracle.cpp"
+    cxx = shutil.which(os.environ.get("CXX", "g++")) or shutil.which("g++")
+    if cxx:
+        tag = hashlib.sha1(src.read_bytes() + " ".join(REF_FLAGS).encode()).hexdigest()[:12]
+        out = Path(out_dir or tempfile.gettempdir()) / f"w2v_cpu_baseline_{tag}.so"
+        if not out.exists():
+            tmp = out.with_suffix(f".{os.getpid()}.so")
+            r = subprocess.run([cxx, *REF_FLAGS, "-fPIC", "-shared", "-o", str(tmp), str(src)],
+                               capture_output=True, text=True)
+            if r.returncode == 0:
+                os.replace(tmp, out)
+        if out.exists():
+            return out, " ".join(REF_FLAGS)
+    return FAST_LIB, " ".join(PORTABLE_FLAGS) + " (prebuilt)"
+
+
+class BaselineLib:
+    """Context for Oracle(..., lib=...): the reference-flags build."""
+
+    def __init__(self, path):
+        self.L = _bind(path)
 
 
 def _p(a):
@@ -87,8 +134,8 @@ class Oracle:
 
     def __init__(self, iter=1, window=5, min_count=5, table_size=100_000_000, word_dim=200, negative=0,
                  subsample_threshold=1e-3, init_alpha=0.025, min_alpha=1e-6, cbow_mean=False,
-                 train_method="hs", model="cbow"):
-        self.L = lib()
+                 train_method="hs", model="cbow", native=None):
+        self.L = native.L if native is not None else lib()
         self.dim = word_dim
         self.hs = train_method == "hs"
         self.cbow = model == "cbow"
@@ -208,8 +255,11 @@ class Oracle:
         """Shared-negatives minibatch skip-gram (configs[4]) for later training calls."""
         self.L.orc_set_shared_negatives(self.h, int(bool(on)))
 
-    def train_omp(self, threads: int, n_sent_limit: int, seed: int = 1) -> int:
-        return self.L.orc_train_omp(self.h, threads, n_sent_limit, seed)
+    def train_omp(self, threads: int, n_sent_limit: int, seed: int = 1, shared_rng: bool = False) -> int:
+        """The reference's OpenMP loop on `threads` threads over the first
+        n_sent_limit sentences; shared_rng = one unsynchronised mt19937 for all
+        threads, as the reference (a data race), else one per thread."""
+        return self.L.orc_train_omp_shared(self.h, threads, n_sent_limit, seed, int(bool(shared_rng)))
 
     def set_vocab_counts(self, counts):
         c = np.ascontiguousarray(counts, np.int64)

@@ -724,8 +724,17 @@ void orc_philox(const uint32_t* ctr, uint64_t key, uint32_t* out) {
 // alpha, but one generator per thread (the shared one is a data race, UB).
 // Trains `n_sent_limit` sentences (a bounded sample) from the current model.
 // Returns the in-vocab words consumed.
+int64_t orc_train_omp_shared(void* h, int32_t threads, int64_t n_sent_limit, uint32_t seed, int32_t shared_rng);
 int64_t orc_train_omp(void* h, int32_t threads, int64_t n_sent_limit, uint32_t seed) {
+  return orc_train_omp_shared(h, threads, n_sent_limit, seed, 0);
+}
+// shared_rng != 0: every thread draws from ONE mt19937, unsynchronised, as the
+// reference does (Word2Vec.h:56 `generator`, used by all OpenMP threads at
+// Word2Vec.cpp:255,282,285,332,335 — a data race, undefined behaviour; kept
+// because it is what the reference build runs and times).
+int64_t orc_train_omp_shared(void* h, int32_t threads, int64_t n_sent_limit, uint32_t seed, int32_t shared_rng) {
   Orc& m = *H(h);
+  std::mt19937 shared_gen(seed);
   const int64_t n = std::min<int64_t>((int64_t)m.off.size() - 1, n_sent_limit);
   int64_t cw = 0;
   float alpha = m.cfg.init_alpha;
@@ -741,7 +750,7 @@ int64_t orc_train_omp(void* h, int32_t threads, int64_t n_sent_limit, uint32_t s
     tid = omp_get_thread_num();
 #endif
     std::mt19937 g(seed + 7919u * (uint32_t)tid);
-    RefDraws dr(&g, m.cfg.window, m.cfg.table_size, nullptr);
+    RefDraws dr(shared_rng ? &shared_gen : &g, m.cfg.window, m.cfg.table_size, nullptr);
 #pragma omp for schedule(static)
     for (int64_t i = 0; i < n; ++i) {
       if (i % 10 == 0) {

@@ -59,7 +59,25 @@ def device_from_oracle(o: Oracle, cfg, initial=True):
 
 
 def rel_err(a, b):
+    """Norm-wise: max |a - b| over the whole matrix / max |b| (a matrix-level bound)."""
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
     den = max(np.abs(b).max(), 1e-30)
     return float(np.abs(a - b).max() / den)
+
+
+def elem_rel_err(a, b, floor_frac=1e-3):
+    """Per-element: max over elements of |a - b| / max(|b|, floor), floor =
+    floor_frac * max |b| (an element far below the matrix's scale, or an exact
+    zero, is compared against that floor instead of its own magnitude, since
+    its own relative error is dominated by the rounding of the larger terms it
+    was summed from)."""
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    floor = max(np.abs(b).max() * floor_frac, 1e-30)
+    return float((np.abs(a - b) / np.maximum(np.abs(b), floor)).max())
+
+
+def errs(a, b):
+    """(norm-wise, per-element) relative error, for messages and logs."""
+    return rel_err(a, b), elem_rel_err(a, b)

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 from tests.corpus import zipf_sentences
-from tests.harness import MODES, device_config, device_from_oracle, oracle_run, rel_err
+from tests.harness import MODES, device_config, device_from_oracle, elem_rel_err, oracle_run, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -52,7 +52,13 @@ def test_replay_single_sentence(mode):
         if np.abs(dw).max() == 0:
             np.testing.assert_array_equal(g, w)
             continue
-        assert rel_err(g - i, dw) < 1e-5, mode
+        # north_star's 1e-5, norm-wise; per element (floor 1e-3 of the largest
+        # delta) the bound is 1e-3: a delta is a sum of g * x terms whose
+        # summation order differs (wave tree vs sequential)
+        e_norm, e_elem = rel_err(g - i, dw), elem_rel_err(g - i, dw)
+        print(f"{mode}: rel_err {e_norm:.2e} per-element {e_elem:.2e}")
+        assert e_norm < 1e-5, mode
+        assert e_elem < 1e-3, mode
 
 
 @pytest.mark.parametrize("mode", list(MODES))
@@ -64,6 +70,46 @@ def test_replay_epoch(mode, dim):
         if w is None:
             continue
         assert rel_err(g - i, w - i) < 1e-4, mode
+
+
+# Every instantiated row width (floats per lane NV = ceil(d / 64): 1, 2, 3, 4,
+# 5, 6, 8, 12, 16; w2v_dev.hip pick_nv), including configs[1]'s d=200 (NV 4),
+# and dims that leave part of the last 64-lane chunk idle.
+NV_DIMS = [40, 100, 150, 200, 300, 350, 512, 700, 1000]
+
+
+@pytest.mark.parametrize("mode", ["sg_ns", "cbow_hs"])
+@pytest.mark.parametrize("dim", NV_DIMS)
+def test_replay_epoch_row_widths(mode, dim):
+    sents = zipf_sentences(8, 160, 300, seed=31, ragged=True)
+    got, want, init = _run_replay(mode, sents, dim=dim, window=5, iters=2)
+    for g, w, i in zip(got, want, init):
+        if w is None:
+            continue
+        assert rel_err(g - i, w - i) < 1e-4, (mode, dim)
+
+
+@pytest.mark.parametrize("mode", ["sg_ns", "cbow_hs"])
+@pytest.mark.parametrize("dim", NV_DIMS)
+def test_philox_sequential_row_widths(mode, dim):
+    sents = zipf_sentences(8, 160, 300, seed=37, ragged=True)
+    o = oracle_run(sents, mode, dim=dim, window=5, iters=1, table_size=100_000, train=False)
+    o.build_sample()
+    cfg = device_config(o, mode, dim, 5, 1, 100_000, True, 0.05, 2.5e-6)
+    d = device_from_oracle(o, cfg, initial=False)
+    init = [o.matrix(k) for k in range(3)]
+    key = 0x0DDB_A11C_AFE0_0001 + dim
+    order = np.random.default_rng(dim).permutation(o.samples()[1].size - 1)
+    o.train_philox(0, 1, order, key, 0)
+    d.set_rng(N.W2V_RNG_PHILOX, key)
+    d.set_schedule(N.W2V_SCHED_SEQUENTIAL)
+    d.set_progress(0)
+    st = d.train_epoch(0, order)
+    assert st["words"] == o.current_words
+    for k, g in enumerate(d.download_model()):
+        if g is not None:
+            assert rel_err(g - init[k], o.matrix(k) - init[k]) < 1e-4, (mode, dim, k)
+    d.close()
 
 
 @pytest.mark.parametrize("mode", list(MODES))
@@ -92,10 +138,12 @@ def test_philox_sequential(mode):
         assert rel_err(g - init[k], w - init[k]) < 1e-4, (mode, k)
 
 
-@pytest.mark.parametrize("mode", ["sg_ns", "cbow_hs"])
-def test_parallel_runs_and_counts(mode):
+@pytest.mark.parametrize("mode,dim", [("sg_ns", 300), ("cbow_hs", 300), ("cbow_hs", 200), ("sg_ns", 100)])
+def test_parallel_runs_and_counts(mode, dim):
+    """Full-concurrency parallel schedule with the default update policy (for
+    CBOW-HS: LDS-private Huffman top nodes and context rows; configs[1] is
+    CBOW-HS d200): size-independent properties."""
     sents = zipf_sentences(400, 300, 2000, seed=11, ragged=True)
-    dim = 300
     o = oracle_run(sents, mode, dim=dim, window=5, iters=1, table_size=1_000_000, train=False)
     o.build_sample()
     cfg = device_config(o, mode, dim, 5, 1, 1_000_000, True, 0.05, 2.5e-6)
@@ -107,6 +155,7 @@ def test_parallel_runs_and_counts(mode):
     ids, off = o.samples()
     assert st["words"] == ids.size
     assert st["sentences"] == off.size - 1
+    assert st["nonfinite"] == 0
     W, Cm, S = d.download_model()
     for m in (W, Cm, S):
         if m is not None:
@@ -198,3 +247,40 @@ def test_window_limit():
     DeviceTrainer(Config(word_dim=16, window=127, negative=5, cbow=True, table_size=1000))
     with pytest.raises(N.DevError, match="window"):
         DeviceTrainer(Config(word_dim=16, window=128, negative=5, table_size=1000))
+
+
+def test_divergence_fails_loudly():
+    """A run whose weights blow up returns W2V_ERR_DIVERGED (the device counts
+    non-finite sigma arguments) instead of reporting success."""
+    sents = zipf_sentences(40, 200, 300, seed=41, ragged=True)
+    o = oracle_run(sents, "sg_ns", dim=64, window=5, iters=1, table_size=100_000, train=False)
+    o.build_sample()
+    cfg = device_config(o, "sg_ns", 64, 5, 1, 100_000, True, 0.05, 2.5e-6)
+    d = device_from_oracle(o, cfg, initial=False)
+    W, Cm, _ = (o.matrix(0), o.matrix(1), None)
+    d.upload_model(W * 1e30, Cm + 1e30)  # sigma arguments overflow to inf on the first update
+    d.set_rng(N.W2V_RNG_PHILOX, 5)
+    d.set_schedule(N.W2V_SCHED_PARALLEL)
+    d.set_progress(0)
+    with pytest.raises(N.DevError) as ei:
+        d.train_epoch(0, None)
+    assert ei.value.code == N.W2V_ERR_DIVERGED
+    assert d.read_stats()["nonfinite"] > 0
+    d.close()
+
+
+def test_experiment_knobs_read_once(monkeypatch):
+    """Experiment environment variables are read at w2v_dev_create and reported;
+    setting one afterwards changes nothing."""
+    from word2vec_amd.device import Config, DeviceTrainer
+
+    for k in ("W2V_SEG_LEN", "W2V_DEBUG_WPB", "W2V_DEBUG_LDS_PER_WAVE", "W2V_DEBUG_MAX_BLOCKS", "W2V_SN_OCC",
+              "W2V_SN_COHERENT_ROWS", "W2V_SN_ATOMIC_ROWS"):
+        monkeypatch.delenv(k, raising=False)
+    d0 = DeviceTrainer(Config(word_dim=16, window=5, negative=5, table_size=1000))
+    monkeypatch.setenv("W2V_SEG_LEN", "64")
+    assert d0.knobs() == ""
+    d1 = DeviceTrainer(Config(word_dim=16, window=5, negative=5, table_size=1000))
+    assert d1.knobs() == "W2V_SEG_LEN=64"
+    d0.close()
+    d1.close()

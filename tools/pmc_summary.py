@@ -52,9 +52,12 @@ def main(tag, key):
         "traffic_GBps": traffic / (float(k["AverageNs"]) * 1e-9) / 1e9,
     }
     (dst / f"{tag}_pmc.json").write_text(json.dumps(rec, indent=1) + "\n")
+    rec["bench_ms_per_step_same_process"] = bench["ms_per_step"]
+    (dst / f"{tag}_pmc.json").write_text(json.dumps(rec, indent=1) + "\n")
     tf = dst / "pmc_traffic.json"
     allrec = json.loads(tf.read_text()) if tf.exists() else {}
-    allrec[key] = int(traffic)
+    allrec[key] = {"traffic": int(traffic), "source": f"profiles/{tag}_pmc.json",
+                   "avg_duration_ms_rocprof": rec["avg_duration_ms_rocprof"]}
     tf.write_text(json.dumps(allrec, indent=1) + "\n")
     print(json.dumps(rec, indent=1))
 

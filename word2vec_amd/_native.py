@@ -15,6 +15,11 @@ LIB_DIR = Path(__file__).resolve().parent / "lib"
 DEV_LIB = LIB_DIR / "libw2v_hip.so"
 
 W2V_OK = 0
+W2V_ERR_ARG = 1
+W2V_ERR_HIP = 2
+W2V_ERR_STATE = 3
+W2V_ERR_UNSUPPORTED = 4
+W2V_ERR_DIVERGED = 5
 W2V_RNG_PHILOX = 0
 W2V_RNG_REPLAY = 1
 W2V_SCHED_PARALLEL = 0
@@ -48,6 +53,7 @@ class DevStats(C.Structure):
         ("targets", C.c_int64),
         ("draws", C.c_int64),
         ("sentences", C.c_int64),
+        ("nonfinite", C.c_int64),
     ]
 
     def as_dict(self):
@@ -64,6 +70,7 @@ _F = C.c_float
 SIGNATURES = {
     "w2v_dev_version": (C.c_char_p, []),
     "w2v_dev_last_error": (C.c_char_p, []),
+    "w2v_dev_knobs": (C.c_char_p, [_P]),
     "w2v_dev_create": (C.c_int, [C.POINTER(DevConfig), C.POINTER(_P)]),
     "w2v_dev_destroy": (None, [_P]),
     "w2v_dev_set_stream": (C.c_int, [_P, _P]),
@@ -120,10 +127,12 @@ def load_dev_lib(path: os.PathLike | str | None = None) -> C.CDLL:
 
 
 class DevError(RuntimeError):
-    pass
+    def __init__(self, msg: str, code: int = 0):
+        super().__init__(msg)
+        self.code = code
 
 
 def check(lib: C.CDLL, rc: int, what: str) -> None:
     if rc != W2V_OK:
         msg = lib.w2v_dev_last_error().decode(errors="replace")
-        raise DevError(f"{what} failed (code {rc}): {msg}")
+        raise DevError(f"{what} failed (code {rc}): {msg}", rc)

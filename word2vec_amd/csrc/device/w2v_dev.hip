@@ -5,6 +5,8 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -63,8 +65,40 @@ void dfree(T*& p) {
 constexpr int64_t kSegLen = 128;
 constexpr int64_t kMaxSeg = 64;
 
+// Experiment knobs (environment variables, read ONCE at w2v_dev_create and
+// reported by w2v_dev_knobs / bench.py's JSON): a stray variable must not
+// change a training run silently. -1 / 0 = not set.
+struct Knobs {
+  int64_t seg_len = -1;          // W2V_SEG_LEN: tokens per work item (0 = whole sentences)
+  int wpb = 0;                   // W2V_DEBUG_WPB: waves per workgroup
+  int64_t lds_per_wave = 0;      // W2V_DEBUG_LDS_PER_WAVE: LDS budget per wave (bytes)
+  int64_t max_blocks = 0;        // W2V_DEBUG_MAX_BLOCKS: grid cap
+  int sn_occ = 0;                // W2V_SN_OCC: shared-negatives kernel's waves per SIMD
+  int64_t sn_coherent_rows = -1; // W2V_SN_COHERENT_ROWS
+  int64_t sn_atomic_rows = -1;   // W2V_SN_ATOMIC_ROWS
+  std::string desc;              // "NAME=value ..." of the variables that were set
+};
+
+static Knobs read_knobs() {
+  Knobs k;
+  auto get = [&](const char* name) -> const char* {
+    const char* v = std::getenv(name);
+    if (v && *v) k.desc += (k.desc.empty() ? "" : " ") + std::string(name) + "=" + v;
+    return (v && *v) ? v : nullptr;
+  };
+  if (const char* v = get("W2V_SEG_LEN")) k.seg_len = std::max<int64_t>(0, std::atoll(v));
+  if (const char* v = get("W2V_DEBUG_WPB")) k.wpb = std::max(1, std::atoi(v));
+  if (const char* v = get("W2V_DEBUG_LDS_PER_WAVE")) k.lds_per_wave = std::max<int64_t>(0, std::atoll(v));
+  if (const char* v = get("W2V_DEBUG_MAX_BLOCKS")) k.max_blocks = std::max<int64_t>(0, std::atoll(v));
+  if (const char* v = get("W2V_SN_OCC")) k.sn_occ = std::max(0, std::atoi(v));
+  if (const char* v = get("W2V_SN_COHERENT_ROWS")) k.sn_coherent_rows = std::max<int64_t>(0, std::atoll(v));
+  if (const char* v = get("W2V_SN_ATOMIC_ROWS")) k.sn_atomic_rows = std::max<int64_t>(0, std::atoll(v));
+  return k;
+}
+
 struct w2v_dev {
   w2v_dev_config cfg{};
+  Knobs knobs;
   int device = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
@@ -110,6 +144,12 @@ struct w2v_dev {
   int n_cu = 256;
   bool model_ready = false, vocab_ready = false, corpus_ready = false;
   bool model_bound = false;  // W/C/S owned by the caller
+  // Host statistics for the privatised rows' flush scales (priv_scales):
+  std::vector<float> keep_h;        // sample probabilities
+  std::vector<double> table_frac;   // unigram-table share of rows [0, kPrivMax)
+  std::vector<int32_t> top_node;    // HS: per word, the deepest node of its path among the kPrivMax nearest the root (-1: none)
+  std::vector<int32_t> node_parent; // HS: parent of node (V - 1 - kPrivMax + j), -1 for the root
+  std::vector<int64_t> tok_count;   // corpus token count per word
 };
 
 namespace {
@@ -168,6 +208,8 @@ extern "C" {
 const char* w2v_dev_version(void) { return "word2vec_amd-dev 0.1 (gfx950)"; }
 const char* w2v_dev_last_error(void) { return g_err.c_str(); }
 
+const char* w2v_dev_knobs(w2v_dev* h) { return h ? h->knobs.desc.c_str() : ""; }
+
 int w2v_dev_create(const w2v_dev_config* cfg, w2v_dev** out) {
   if (!cfg || !out) return fail(W2V_ERR_ARG, "w2v_dev_create: null argument");
   *out = nullptr;
@@ -183,6 +225,7 @@ int w2v_dev_create(const w2v_dev_config* cfg, w2v_dev** out) {
   if (cfg->iter <= 0) return fail(W2V_ERR_ARG, "iter must be > 0");
   w2v_dev* h = new w2v_dev();
   h->cfg = *cfg;
+  h->knobs = read_knobs();
   if (cfg->device >= 0) {
     h->device = cfg->device;
   } else {
@@ -266,53 +309,92 @@ int w2v_dev_upload_vocab(w2v_dev* h, int64_t V, const float* keep, const int64_t
   if (h->cfg.negative > 0 && !bounds && !h->table)
     return fail(W2V_ERR_ARG, "negative sampling needs table_bounds (or w2v_dev_upload_table first)");
   if (h->cfg.hs && (!codes || !points || !coff)) return fail(W2V_ERR_ARG, "hs needs codes/points/code_offsets");
+  // validate everything before touching the handle, so a rejected call leaves it as it was
+  const int64_t n = h->cfg.table_size;
+  if (h->cfg.negative > 0 && bounds) {
+    if (bounds[0] != 0 || bounds[V] != n) return fail(W2V_ERR_ARG, "table_bounds must start at 0 and end at table_size");
+    for (int64_t w = 0; w < V; ++w)
+      if (bounds[w] > bounds[w + 1]) return fail(W2V_ERR_ARG, "table_bounds must be non-decreasing");
+  }
+  if (h->cfg.hs) {
+    if (coff[0] != 0) return fail(W2V_ERR_ARG, "code_offsets[0] must be 0");
+    for (int64_t w = 0; w < V; ++w)
+      if (coff[w] > coff[w + 1] || coff[w + 1] - coff[w] > 4096)
+        return fail(W2V_ERR_ARG, "code_offsets must be non-decreasing with paths <= 4096");
+    for (int64_t t = 0; t < coff[V]; ++t)
+      if (points[t] < 0 || points[t] > V - 2 || codes[t] > 1)
+        return fail(W2V_ERR_ARG, "Huffman point/code out of range");
+  }
   if (set_device(h)) return W2V_ERR_HIP;
+  // device buffers first (a HIP failure leaves the handle's old vocab in place)
+  float* dkeep = nullptr;
+  uint32_t* dtable = nullptr;
+  int64_t* db = nullptr;
+  uint8_t* dcodes = nullptr;
+  int32_t* dpoints = nullptr;
+  int64_t* dcoff = nullptr;
+  auto drop = [&]() { dfree(dkeep); dfree(dtable); dfree(db); dfree(dcodes); dfree(dpoints); dfree(dcoff); };
+  hipError_t e = hipMalloc(&dkeep, V * sizeof(float));
+  if (e == hipSuccess) e = hipMemcpy(dkeep, keep, V * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess && h->cfg.negative > 0 && bounds) {
+    e = hipMalloc(&dtable, n * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&db, (V + 1) * sizeof(int64_t));
+    if (e == hipSuccess) e = hipMemcpy(db, bounds, (V + 1) * sizeof(int64_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(w2v::expand_table_kernel, dim3(4096), dim3(256), 0, h->stream, db, V, dtable, n);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  }
+  const int64_t nc = h->cfg.hs ? coff[V] : 0;
+  if (e == hipSuccess && h->cfg.hs) {
+    e = hipMalloc(&dcodes, (nc > 0 ? nc : 1));
+    if (e == hipSuccess) e = hipMalloc(&dpoints, (nc > 0 ? nc : 1) * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc(&dcoff, (V + 1) * sizeof(int64_t));
+    if (e == hipSuccess && nc > 0) e = hipMemcpy(dcodes, codes, nc, hipMemcpyHostToDevice);
+    if (e == hipSuccess && nc > 0) e = hipMemcpy(dpoints, points, nc * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dcoff, coff, (V + 1) * sizeof(int64_t), hipMemcpyHostToDevice);
+  }
+  if (e != hipSuccess) {
+    drop();
+    return fail(W2V_ERR_HIP, std::string("w2v_dev_upload_vocab: ") + hipGetErrorString(e));
+  }
+  dfree(db);
   if (h->V != V) {
     if (!h->model_bound) { dfree(h->W); dfree(h->C); dfree(h->S); }
     h->W = h->C = h->S = nullptr;
     h->model_bound = false;
     h->pitch = (h->cfg.word_dim + 63) & ~63;
     h->model_ready = false;
+    h->tok_count.clear();  // the corpus statistics refer to the old ids
   }
   h->V = V;
   dfree(h->keep);
-  HIP_TRY(hipMalloc(&h->keep, V * sizeof(float)));
-  HIP_TRY(hipMemcpy(h->keep, keep, V * sizeof(float), hipMemcpyHostToDevice));
-  if (h->cfg.negative > 0 && bounds) {
-    const int64_t n = h->cfg.table_size;
-    if (bounds[0] != 0 || bounds[V] != n) return fail(W2V_ERR_ARG, "table_bounds must start at 0 and end at table_size");
-    for (int64_t w = 0; w < V; ++w)
-      if (bounds[w] > bounds[w + 1]) return fail(W2V_ERR_ARG, "table_bounds must be non-decreasing");
-    int64_t* db = nullptr;
+  h->keep = dkeep;
+  h->keep_h.assign(keep, keep + V);
+  if (dtable) {
     dfree(h->table);
-    HIP_TRY(hipMalloc(&h->table, n * sizeof(uint32_t)));
-    HIP_TRY(hipMalloc(&db, (V + 1) * sizeof(int64_t)));
-    HIP_TRY(hipMemcpy(db, bounds, (V + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(w2v::expand_table_kernel, dim3(4096), dim3(256), 0, h->stream, db, V,
-                       h->table, n);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    HIP_TRY(hipFree(db));
+    h->table = dtable;
+    h->table_frac.assign((size_t)std::min<int64_t>(V, w2v::kPrivMax), 0.0);
+    for (size_t r = 0; r < h->table_frac.size(); ++r) h->table_frac[r] = (double)(bounds[r + 1] - bounds[r]) / (double)n;
   }
   if (h->cfg.hs) {
-    for (int64_t w = 0; w < V; ++w)
-      if (coff[w] > coff[w + 1] || coff[w + 1] - coff[w] > 4096)
-        return fail(W2V_ERR_ARG, "code_offsets must be non-decreasing with paths <= 4096");
-    if (coff[0] != 0) return fail(W2V_ERR_ARG, "code_offsets[0] must be 0");
-    const int64_t nc = coff[V];
-    for (int64_t t = 0; t < nc; ++t)
-      if (points[t] < 0 || points[t] > V - 2 || codes[t] > 1)
-        return fail(W2V_ERR_ARG, "Huffman point/code out of range");
     dfree(h->codes); dfree(h->points); dfree(h->coff);
-    HIP_TRY(hipMalloc(&h->codes, (nc > 0 ? nc : 1)));
-    HIP_TRY(hipMalloc(&h->points, (nc > 0 ? nc : 1) * sizeof(int32_t)));
-    HIP_TRY(hipMalloc(&h->coff, (V + 1) * sizeof(int64_t)));
-    if (nc > 0) {
-      HIP_TRY(hipMemcpy(h->codes, codes, nc, hipMemcpyHostToDevice));
-      HIP_TRY(hipMemcpy(h->points, points, nc * sizeof(int32_t), hipMemcpyHostToDevice));
-    }
-    HIP_TRY(hipMemcpy(h->coff, coff, (V + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+    h->codes = dcodes; h->points = dpoints; h->coff = dcoff;
     h->n_codes = nc;
+    // the kPrivMax internal nodes nearest the root (ids V-1-kPrivMax .. V-2;
+    // a node is created after its children, so the range is closed upwards)
+    const int64_t lo = std::max<int64_t>(0, V - 1 - w2v::kPrivMax);
+    h->top_node.assign((size_t)V, -1);
+    h->node_parent.assign((size_t)(V - 1 - lo), -1);
+    for (int64_t w = 0; w < V; ++w) {
+      int32_t prev = -1;
+      for (int64_t t = coff[w]; t < coff[w + 1] && points[t] >= lo; ++t) {  // paths run root -> leaf
+        h->node_parent[(size_t)(points[t] - lo)] = prev;
+        prev = points[t];
+      }
+      h->top_node[(size_t)w] = prev;
+    }
   }
   h->vocab_ready = true;
   return W2V_OK;
@@ -325,6 +407,9 @@ int w2v_dev_upload_table(w2v_dev* h, const uint32_t* table, int64_t n) {
   dfree(h->table);
   HIP_TRY(hipMalloc(&h->table, n * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(h->table, table, n * sizeof(uint32_t), hipMemcpyHostToDevice));
+  h->table_frac.assign(w2v::kPrivMax, 0.0);
+  for (int64_t i = 0; i < n; ++i)
+    if (table[i] < (uint32_t)w2v::kPrivMax) h->table_frac[table[i]] += 1.0 / (double)n;
   return W2V_OK;
 }
 
@@ -423,8 +508,11 @@ int w2v_dev_upload_corpus(w2v_dev* h, const int32_t* ids, int64_t n_tok, const i
     max_len = std::max<int64_t>(max_len, soff[s + 1] - soff[s]);
   }
   if (h->V < 1) return fail(W2V_ERR_STATE, "upload the vocab before the corpus");
-  for (int64_t t = 0; t < n_tok; ++t)
+  std::vector<int64_t> hist((size_t)h->V, 0);  // also the flush-scale statistics (priv_scales)
+  for (int64_t t = 0; t < n_tok; ++t) {
     if (ids[t] < 0 || ids[t] >= h->V) return fail(W2V_ERR_ARG, "token id out of vocab range");
+    ++hist[(size_t)ids[t]];
+  }
   if (train_words <= 0 && n_tok > 0) return fail(W2V_ERR_ARG, "train_words must be > 0");
   if (set_device(h)) return W2V_ERR_HIP;
   dfree(h->ids); dfree(h->soff); dfree(h->order);
@@ -437,6 +525,7 @@ int w2v_dev_upload_corpus(w2v_dev* h, const int32_t* ids, int64_t n_tok, const i
   h->n_sent = n_sent;
   h->max_len = max_len;
   h->train_words = train_words;
+  h->tok_count.swap(hist);
   h->corpus_ready = true;
   return W2V_OK;
 }
@@ -477,6 +566,72 @@ int w2v_dev_get_progress(w2v_dev* h, int64_t* cw) {
 
 static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int64_t count);
 
+// Flush scales of the privatised rows (flush_private / sn_flush_private): a
+// row that n of the launch's G workgroups update within one flush interval of
+// k workgroup centers gets its summed delta scaled by 1 / max(1, n / S), S =
+// priv_avg. n is the EXPECTED count, G (1 - exp(-k m)), with m the row's
+// expected updates per center from the corpus and vocab statistics — a fixed
+// function of the row's frequency rank, so the scale does not depend on the
+// schedule (the previous estimator, each workgroup's running fraction of
+// flushes that found the row dirty, was noisy early in a launch). Per kept
+// center, with f(w) = token share, fk(w) = kept-center share, u(w) = unigram
+// table share, and window + 1 the expected number of context positions
+// (Word2Vec.cpp:335-337: b = window - U[0, window-1]):
+//   SG-NS output (C) rows  (window + 1) (f(r) + neg u(r))   positives are contexts (:346-349)
+//   CBOW-NS output (W)     fk(r) + neg u(r)                  positive is the center (:310)
+//   shared negatives (C)   fk(r) + neg u(r)                  center + the window's shared draws
+//   SG-HS nodes            (window + 1) sum_{w below} f(w)   every context's path (:342-345)
+//   CBOW-HS nodes          sum_{w below} fk(w)               the center's path (:304-306)
+//   CBOW context (C) rows  (window + 1) f(r)                 window positions (:288-300)
+static void priv_scales(const w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool shared) {
+  for (int p = 0; p < w2v::kPrivMax; ++p) a.priv_sc[p] = 1.0f;
+  for (int p = 0; p < w2v::kCtxMax; ++p) a.ctx_sc[p] = 1.0f;
+  if (!(a.priv_avg > 0.0f) || (a.priv_n == 0 && a.ctx_n == 0)) return;
+  const double S = a.priv_avg, win1 = (double)h->cfg.window + 1.0, neg = (double)h->cfg.negative;
+  const int64_t V = h->V;
+  double N = 0.0, K = 0.0;
+  const bool have = (int64_t)h->tok_count.size() == V && (int64_t)h->keep_h.size() == V;
+  if (have)
+    for (int64_t w = 0; w < V; ++w) {
+      N += (double)h->tok_count[(size_t)w];
+      K += (double)h->tok_count[(size_t)w] * std::min(1.0, (double)h->keep_h[(size_t)w]);
+    }
+  auto sc = [&](double m, int k) {
+    const double n = (N > 0.0 && K > 0.0) ? (double)G * (1.0 - std::exp(-(double)k * m)) : (double)G;
+    return (float)(1.0 / std::max(1.0, n / S));
+  };
+  auto f = [&](int64_t r) { return N > 0.0 ? (double)h->tok_count[(size_t)r] / N : 0.0; };
+  auto fk = [&](int64_t r) {
+    return K > 0.0 ? (double)h->tok_count[(size_t)r] * std::min(1.0, (double)h->keep_h[(size_t)r]) / K : 0.0;
+  };
+  auto u = [&](int64_t r) { return r < (int64_t)h->table_frac.size() ? h->table_frac[(size_t)r] : 0.0; };
+  const bool cbow = h->cfg.cbow != 0;
+  if (a.priv_n > 0) {
+    if (!shared && h->cfg.hs) {
+      const int64_t lo = std::max<int64_t>(0, V - 1 - w2v::kPrivMax);
+      std::vector<double> acc(h->node_parent.size(), 0.0);
+      if (have && h->top_node.size() == (size_t)V) {
+        for (int64_t w = 0; w < V; ++w)
+          if (h->top_node[(size_t)w] >= 0) acc[(size_t)(h->top_node[(size_t)w] - lo)] += cbow ? fk(w) : f(w);
+        for (size_t j = 0; j < acc.size(); ++j)  // children have lower ids than their parents
+          if (h->node_parent[j] >= 0) acc[(size_t)(h->node_parent[j] - lo)] += acc[j];
+      }
+      for (int p = 0; p < a.priv_n; ++p) {
+        const int64_t j = a.priv_lo + p - lo;
+        const double m = (j >= 0 && j < (int64_t)acc.size()) ? acc[(size_t)j] : 1.0;
+        a.priv_sc[p] = sc(cbow ? m : win1 * m, a.flush_every);
+      }
+    } else {
+      for (int p = 0; p < a.priv_n; ++p) {
+        const int64_t r = a.priv_lo + p;
+        const double m = (shared || cbow) ? fk(r) + neg * u(r) : win1 * (f(r) + neg * u(r));
+        a.priv_sc[p] = sc(m, a.flush_every);
+      }
+    }
+  }
+  for (int p = 0; p < a.ctx_n; ++p) a.ctx_sc[p] = sc(win1 * f(p), a.ctx_flush_every);
+}
+
 // The shared-negatives minibatch covers skip-gram NS only: a 16 x 16 MFMA tile
 // holds <= 16 unique context rows (2 * window <= 16) and the center + <= 15
 // negatives; its draws are Philox (the reference has no such path to replay).
@@ -515,8 +670,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   int sn_waves = 0;
   if (h->update == W2V_UPDATE_SHARED_NEGATIVES) {
     if (int rc = check_shared_negatives(h, true)) return rc;
-    int occ = 0;  // register budget (waves per SIMD); experiment knob
-    if (const char* e = std::getenv("W2V_SN_OCC")) occ = std::atoi(e);
+    const int occ = h->knobs.sn_occ;  // register budget (waves per SIMD); experiment knob
     if ((double)h->V * (double)h->pitch * sizeof(float) >= 4294967296.0)
       return fail(W2V_ERR_UNSUPPORTED, "shared negatives: W / C must be < 4 GiB each (32-bit buffer offsets)");
     if (!(sn_fn = w2v::pick_shared_neg(h->pitch, occ, &sn_waves)))
@@ -551,7 +705,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   // under a wave cap, narrower workgroups so the capped grid still spans the CUs.
   const int max_wpb = (h->nv <= 6 ? 1024 : 256) / w2v::kWave;
   int wpb = max_wpb;
-  if (const char* e = std::getenv("W2V_DEBUG_WPB")) wpb = std::max(1, std::min(max_wpb, std::atoi(e)));  // experiments
+  if (h->knobs.wpb > 0) wpb = std::min(max_wpb, h->knobs.wpb);  // experiments
   if (h->max_waves > 0) {
     int64_t per = h->max_waves / (h->n_cu > 0 ? h->n_cu : 1);
     wpb = 1;
@@ -583,7 +737,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   if (h->sched == W2V_SCHED_PARALLEL) {  // the reference-exact schedule keeps per-update rounding
     const int64_t row_bytes = (int64_t)h->nv * w2v::kWave * (int64_t)sizeof(float);
     int64_t per_wave = 10 * 1024;
-    if (const char* e = std::getenv("W2V_DEBUG_LDS_PER_WAVE")) per_wave = std::atoll(e);  // experiments
+    if (h->knobs.lds_per_wave > 0) per_wave = h->knobs.lds_per_wave;  // experiments
     const int64_t budget =
         std::min<int64_t>(160 * 1024, per_wave * (int64_t)wpb) - 4 * w2v::lds_header_words(w2v::kPrivMax, 64);
     int64_t fit = budget / row_bytes;
@@ -604,7 +758,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     // corpus scores; for CBOW-NS (hot rows privatised on both sides of every
     // dot product) it fails the similarity gate at every flush interval tried
     // (profiles/r01_context_rows.log).
-    int64_t Q = h->cfg.cbow ? std::min<int64_t>({fit - P, (int64_t)64, h->V}) : 0;
+    int64_t Q = h->cfg.cbow ? std::min<int64_t>({fit - P, (int64_t)w2v::kCtxMax, h->V}) : 0;
     if (h->context_rows < 0 && !h->cfg.hs) Q = 0;
     if (h->context_rows >= 0) Q = std::min<int64_t>(Q, h->context_rows);
     if (Q > 0) {
@@ -637,11 +791,11 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     // -1, else at least the rows two XCD L2s' capacity could keep resident
     const int64_t l2_rows = (int64_t)(8 << 20) / (h->pitch * (int64_t)sizeof(float));
     a.hot_wc = h->hot_rows < 0 ? h->V : std::min<int64_t>(h->V, std::max<int64_t>(h->hot_rows, l2_rows));
-    if (const char* e = std::getenv("W2V_SN_COHERENT_ROWS")) a.hot_wc = std::min<int64_t>(h->V, std::atoll(e));  // experiments
+    if (h->knobs.sn_coherent_rows >= 0) a.hot_wc = std::min<int64_t>(h->V, h->knobs.sn_coherent_rows);  // experiments
     // the hot_rows most frequent rows take atomic deltas, as in the per-pair
     // kernel (parallel schedule only: the sequential one is exact either way)
     a.hot_atomic = h->sched == W2V_SCHED_PARALLEL ? std::min<int64_t>(h->V, h->hot_rows < 0 ? h->V : h->hot_rows) : 0;
-    if (const char* e = std::getenv("W2V_SN_ATOMIC_ROWS")) a.hot_atomic = std::min<int64_t>(h->V, std::atoll(e));  // experiments
+    if (h->knobs.sn_atomic_rows >= 0) a.hot_atomic = std::min<int64_t>(h->V, h->knobs.sn_atomic_rows);  // experiments
     int64_t g = 1;
     if (h->sched == W2V_SCHED_PARALLEL) {
       int per_cu = 0;
@@ -655,6 +809,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
       g = std::min<int64_t>((int64_t)per_cu * h->n_cu, count);
       if (h->max_waves > 0) g = std::max<int64_t>(1, std::min<int64_t>(g, h->max_waves / sn_waves));
     }
+    priv_scales(h, a, g, true);
     HIP_TRY(hipMemsetAsync(h->work, 0, sizeof(unsigned int), h->stream));
     hipLaunchKernelGGL(sn_fn, dim3((unsigned)g), dim3(threads), 0, h->stream, a);
     HIP_TRY(hipGetLastError());
@@ -672,10 +827,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     const int64_t need = (count + wpb - 1) / wpb;
     int64_t g = need < resident ? need : resident;
     if (h->max_waves > 0 && (h->max_waves + wpb - 1) / wpb < g) g = (h->max_waves + wpb - 1) / wpb;
-    if (const char* cap = std::getenv("W2V_DEBUG_MAX_BLOCKS")) {  // diagnostics only
-      const int64_t c = std::atoll(cap);
-      if (c > 0 && c < g) g = c;
-    }
+    if (h->knobs.max_blocks > 0 && h->knobs.max_blocks < g) g = h->knobs.max_blocks;  // diagnostics only
     grid = dim3((unsigned)g);
     block = dim3(threads);
   }
@@ -691,7 +843,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   a.seg_len = 0;
   if (h->sched == W2V_SCHED_PARALLEL && h->rng == W2V_RNG_PHILOX && count >= (int64_t)grid.x * block.x / w2v::kWave) {
     int64_t seg = kSegLen;
-    if (const char* e = std::getenv("W2V_SEG_LEN")) seg = std::atoll(e);  // experiments; 0 = whole sentences
+    if (h->knobs.seg_len >= 0) seg = h->knobs.seg_len;  // experiments; 0 = whole sentences
     if (seg > 0) {
       seg = (seg + w2v::kWave - 1) / w2v::kWave * w2v::kWave;
       int64_t nseg = (h->max_len + seg - 1) / seg;
@@ -708,6 +860,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
       }
     }
   }
+  priv_scales(h, a, grid.x, false);
   hipLaunchKernelGGL(fn, grid, block, lds_bytes, h->stream, a);
   HIP_TRY(hipGetLastError());
   return W2V_OK;
@@ -716,7 +869,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
 int w2v_dev_train_epoch(w2v_dev* h, int32_t epoch, const int64_t* order, w2v_dev_stats* st) {
   if (!h) return fail(W2V_ERR_ARG, "null handle");
   w2v_dev_stats before{};
-  if (st) {
+  {
     int rc = w2v_dev_read_stats(h, &before);
     if (rc) return rc;
   }
@@ -731,17 +884,22 @@ int w2v_dev_train_epoch(w2v_dev* h, int32_t epoch, const int64_t* order, w2v_dev
   int rc = w2v_dev_train_epoch_async(h, epoch, od);
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(h->stream));
+  w2v_dev_stats after{};
+  rc = w2v_dev_read_stats(h, &after);
+  if (rc) return rc;
   if (st) {
-    w2v_dev_stats after{};
-    rc = w2v_dev_read_stats(h, &after);
-    if (rc) return rc;
     st->words += after.words - before.words;
     st->centers += after.centers - before.centers;
     st->contexts += after.contexts - before.contexts;
     st->targets += after.targets - before.targets;
     st->draws += after.draws - before.draws;
     st->sentences += after.sentences - before.sentences;
+    st->nonfinite += after.nonfinite - before.nonfinite;
   }
+  if (after.nonfinite > before.nonfinite)
+    return fail(W2V_ERR_DIVERGED, "training diverged: " + std::to_string(after.nonfinite - before.nonfinite) +
+                                      " non-finite sigma arguments (row . input) in this epoch; "
+                                      "lower init_alpha or use a less aggressive update policy");
   return W2V_OK;
 }
 
@@ -764,6 +922,7 @@ int w2v_dev_read_stats(w2v_dev* h, w2v_dev_stats* st) {
   st->targets = (int64_t)c[3];
   st->draws = (int64_t)c[4];
   st->sentences = (int64_t)c[5];
+  st->nonfinite = (int64_t)c[6];
   return W2V_OK;
 }
 

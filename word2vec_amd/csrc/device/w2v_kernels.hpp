@@ -102,6 +102,11 @@ struct TrainArgs {
   int64_t hot_atomic;          // shared-negatives kernel: W / C rows [0, hot_atomic) take memory-side atomic deltas
   int32_t nseg;                // work items per sentence (parallel Philox schedule; 1 = whole sentences)
   int32_t seg_len;             // tokens per item when nseg > 1 (a multiple of 64)
+  // Flush scales of the privatised rows (flush_private), computed on the host
+  // per launch from the corpus statistics (launch_train, priv_scales): row p of
+  // the output range gets priv_sc[p], row p of the context range ctx_sc[p].
+  float priv_sc[128];          // kPrivMax
+  float ctx_sc[64];            // kCtxMax
 };
 
 // LDS the shared-negatives kernel gives its private C rows (w2v_shared.hpp kSnPriv; <= 32 rows).
@@ -110,6 +115,14 @@ constexpr int kSnPrivBytes = 16 * 1024;
 struct Counters {
   unsigned long long centers = 0, contexts = 0, targets = 0, draws = 0, sentences = 0;
 };
+
+// stats[kNonFinite] counts sigma arguments (row . input dot products) that
+// were not finite: the model diverged (w2v_dev_train_epoch returns
+// W2V_ERR_DIVERGED). Wave-uniform check, one atomic per offending update.
+constexpr int kNonFinite = 5;
+__device__ __forceinline__ void note_nonfinite(unsigned long long* stats, bool bad, int lane) {
+  if (bad && lane == 0) atomicAdd(stats + kNonFinite, 1ull);
+}
 
 // ---------------------------------------------------------------------------
 // Wave primitives
@@ -175,25 +188,22 @@ __device__ __forceinline__ uint32_t philox_table_pos(const TrainArgs& a, uint32_
 // ---------------------------------------------------------------------------
 // LDS-privatised rows of the per-pair kernel (when priv_n + ctx_n > 0), per workgroup:
 //   words [0,4) dirty mask of the output rows (2 x 64 bits), [4,8) of the
-//   context rows, [8] centers of the workgroup, [9] / [10] flushes of either
-//   range, [11] unused, [12, 12 + priv_n) and [12 + priv_n, 12 + priv_n +
-//   ctx_n) per-row flush hits, then (from lds_header_words) the pending
-//   deltas: priv_n output rows, then ctx_n context rows, NV * 64 floats each.
-//   Each range holds at most kPrivMax rows.
+//   context rows, [8] centers of the workgroup, [9, 16) unused, then (from
+//   lds_header_words) the pending deltas: priv_n output rows, then ctx_n
+//   context rows, NV * 64 floats each. The output range holds at most
+//   kPrivMax rows, the context range kCtxMax.
 // ---------------------------------------------------------------------------
 constexpr int kPrivMax = 128;
-__host__ __device__ inline int64_t lds_header_words(int64_t priv_n, int64_t ctx_n) {
-  return (12 + priv_n + ctx_n + 3) & ~int64_t(3);
-}
+constexpr int kCtxMax = 64;
+__host__ __device__ inline int64_t lds_header_words(int64_t, int64_t) { return 16; }
 
 struct PrivRows {  // one privatised row range [lo, lo + n) of matrix M (n == 0: none)
   float* delta = nullptr;
   unsigned long long* dirty = nullptr;
-  unsigned* flushes = nullptr;
-  unsigned* hits = nullptr;
   float* M = nullptr;
   int64_t lo = 0;
   int n = 0;
+  bool ctx = false;  // the context range (flush scales a.ctx_sc) or the output range (a.priv_sc)
   __device__ bool has(int64_t row) const { return row >= lo && row < lo + n; }
 };
 
@@ -201,10 +211,7 @@ template <int NV>
 __device__ __forceinline__ PrivRows out_rows(const TrainArgs& a, float* lds) {
   PrivRows p;
   if (lds == nullptr || a.priv_n == 0) return p;
-  unsigned* u = reinterpret_cast<unsigned*>(lds);
   p.dirty = reinterpret_cast<unsigned long long*>(lds);
-  p.flushes = u + 9;
-  p.hits = u + 12;
   p.delta = lds + lds_header_words(a.priv_n, a.ctx_n);
   p.M = const_cast<float*>(a.priv_M);
   p.lo = a.priv_lo;
@@ -216,14 +223,12 @@ template <int NV>
 __device__ __forceinline__ PrivRows ctx_rows(const TrainArgs& a, float* lds) {
   PrivRows p;
   if (lds == nullptr || a.ctx_n == 0) return p;
-  unsigned* u = reinterpret_cast<unsigned*>(lds);
   p.dirty = reinterpret_cast<unsigned long long*>(lds + 4);
-  p.flushes = u + 10;
-  p.hits = u + 12 + a.priv_n;
   p.delta = lds + lds_header_words(a.priv_n, a.ctx_n) + (int64_t)a.priv_n * (NV * kWave);
   p.M = const_cast<float*>(a.ctx_M);
   p.lo = 0;
   p.n = a.ctx_n;
+  p.ctx = true;
   return p;
 }
 
@@ -311,7 +316,8 @@ __device__ __forceinline__ void priv_add(const PrivRows& pr, int64_t row, int d,
 template <int NV, int MAXT, bool HSF>
 __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, int lane, int T, int row_l,
                                               int code_l, int t0, const float (&x)[NV], float (&g)[NV],
-                                              float alpha, int64_t hot_lo, int64_t hot_hi, const PrivRows& pr) {
+                                              float alpha, int64_t hot_lo, int64_t hot_hi, const PrivRows& pr,
+                                              unsigned long long* stats) {
   float r[MAXT][NV];
   int rows[MAXT];
   bool hot[MAXT], priv[MAXT];
@@ -343,6 +349,7 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
   for (int t = 0; t < MAXT; ++t) {
     if (t < T) {
       const int code = readlane_i(code_l, t0 + t);
+      if (stats) note_nonfinite(stats, !__builtin_isfinite(f[t]), lane);
       const float e = expf(-f[t]);
       float gt;
       if (HSF) {
@@ -376,6 +383,15 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
 // with atomic swaps, so an add racing the flush from another wave of the
 // workgroup is neither lost nor flushed twice (its dirty bit is set after its
 // adds and survives until the next flush).
+//
+// Scale: a row that n workgroups update within one flush interval receives
+// the mean of their deltas scaled to at most priv_avg concurrent
+// contributions (local SGD on the few rows every wave updates; without it
+// ~10^4 concurrent stale updates of those rows diverge). n is the expected
+// count, computed on the host from the corpus statistics (launch_train:
+// n = workgroups x P(a workgroup touches the row in flush_every centers)), so
+// the scale is a fixed function of the row's frequency rank, not of the
+// schedule (a.priv_sc / a.ctx_sc; 1 when priv_avg == 0).
 template <int NV>
 __device__ __forceinline__ void flush_private(const TrainArgs& a, const PrivRows& pr, int lane) {
   if (pr.n == 0) return;
@@ -387,29 +403,11 @@ __device__ __forceinline__ void flush_private(const TrainArgs& a, const PrivRows
     mw[w] = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(m >> 32)) << 32) |
             (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)m);
   }
-  if ((mw[0] | mw[1]) == 0) return;
-  // Averaging (priv_avg = S > 0): a row that n workgroups update within one
-  // flush interval receives the mean of their deltas scaled to at most S
-  // concurrent contributions (local SGD on the few rows every wave updates),
-  // with n = workgroups x this workgroup's fraction of flushes touching it.
-  float flushes = 1.0f;
-  if (a.priv_avg > 0.0f) {
-    unsigned fl = 0;
-    if (lane == 0) fl = atomicAdd(pr.flushes, 1u) + 1u;
-    flushes = (float)(unsigned)__builtin_amdgcn_readfirstlane((int)fl);
-  }
   for (int w = 0; w < 2; ++w)
   for (unsigned long long m = mw[w]; m;) {
     const int p = 64 * w + __builtin_ctzll(m);
     m &= m - 1;
-    float sc = 1.0f;
-    if (a.priv_avg > 0.0f) {
-      unsigned h = 0;
-      if (lane == 0) h = atomicAdd(pr.hits + p, 1u) + 1u;
-      const float hits = (float)(unsigned)__builtin_amdgcn_readfirstlane((int)h);
-      const float n = (float)gridDim.x * hits / flushes;
-      sc = 1.0f / fmaxf(1.0f, n / a.priv_avg);
-    }
+    const float sc = pr.ctx ? a.ctx_sc[p & (kCtxMax - 1)] : a.priv_sc[p];
     float* q = pr.delta + p * (NV * kWave) + lane;
     float* dst = pr.M + (pr.lo + p) * a.pitch + lane;
 #pragma unroll
@@ -437,7 +435,7 @@ __device__ __forceinline__ void hs_word(const TrainArgs& a, int word, int lane, 
     for (int t0 = 0; t0 < rem; t0 += MAXT) {
       if (a.strict) drain_vmem();
       apply_targets<NV, MAXT, true>(a.S, a.pitch, a.dim, lane, min(MAXT, rem - t0), pt_l, cd_l, t0, x, g,
-                                    alpha, a.hot_s, INT64_MAX, pr);
+                                    alpha, a.hot_s, INT64_MAX, pr, a.stats);
     }
     cnt.targets += (unsigned long long)rem;
   }
@@ -475,7 +473,7 @@ __device__ __forceinline__ void apply_list(const TrainArgs& a, float* M, int T, 
   for (int t0 = 0; t0 < T; t0 += MAXT) {
     if (a.strict) drain_vmem();
     apply_targets<NV, MAXT, false>(M, a.pitch, a.dim, lane_id(), min(MAXT, T - t0), tgt_l, code_l, t0, x, g, alpha,
-                                   0, a.hot_wc, pr);
+                                   0, a.hot_wc, pr, a.stats);
   }
   cnt.targets += (unsigned long long)T;
 }
@@ -864,9 +862,9 @@ __global__ __launch_bounds__(64) void apply_rows_kernel(float* M, int64_t pitch,
   for (int t = 0; t < n; ++t) {
     const int code = (int)codes[t];
     if (hs_form)
-      apply_targets<NV, 1, true>(M, pitch, d, lane, 1, t, code, 0, x, g, alpha, 0, 0, PrivRows());
+      apply_targets<NV, 1, true>(M, pitch, d, lane, 1, t, code, 0, x, g, alpha, 0, 0, PrivRows(), nullptr);
     else
-      apply_targets<NV, 1, false>(M, pitch, d, lane, 1, t, code, 0, x, g, alpha, 0, 0, PrivRows());
+      apply_targets<NV, 1, false>(M, pitch, d, lane, 1, t, code, 0, x, g, alpha, 0, 0, PrivRows(), nullptr);
   }
 #pragma unroll
   for (int v = 0; v < NV; ++v) {

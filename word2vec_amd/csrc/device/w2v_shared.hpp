@@ -297,6 +297,12 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<KB, NW>& 
 #pragma unroll
   for (int w = 1; w < NW; ++w) L += sh.part[par][w][lane];
   par ^= 1;
+  if (wave == 0 && out_ok && 4 * q < M) {  // divergence: a non-finite sigma argument (kNonFinite)
+    bool bad = false;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bad = bad || (4 * q + r < M && !__builtin_isfinite(L[r]));
+    if (bad) atomicAdd(a.stats + kNonFinite, 1ull);
+  }
   f32x4 Ea;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -392,29 +398,21 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<KB, NW>& 
 
 // Move this wave's columns of its dirty private rows' pending deltas into C
 // with memory-side float atomics (no update lost between workgroups) and clear
-// them. As in the per-pair kernel's flush_private (w2v_kernels.hpp), with
-// priv_avg = S > 0 a row that n workgroups update within one flush interval
-// gets its delta scaled to at most S concurrent contributions, n = workgroups
-// x the fraction of this wave's flushes in which the row was dirty (hits_l:
-// lane r counts row r's).
+// them, each row scaled by a.priv_sc (the per-pair kernel's flush_private
+// averaging, w2v_kernels.hpp: a fixed function of the row's frequency rank,
+// computed on the host per launch).
 template <int KB, int NW>
 __device__ __forceinline__ void sn_flush_private(const TrainArgs& a, SnShared<KB, NW>& sh, int wave, int lane,
-                                                 unsigned& dirty, unsigned& flushes, unsigned& hits_l) {
+                                                 unsigned& dirty) {
   constexpr int kCols = KB * kSnTile;  // this wave's columns of a row
   unsigned m = (unsigned)__builtin_amdgcn_readfirstlane((int)dirty);
   dirty = 0;
   if (m == 0) return;
-  flushes += 1;
-  if (lane < 32 && ((m >> lane) & 1u)) hits_l += 1;
   wave_lds_order();
   while (m) {
     const int r = __builtin_ctz(m);
     m &= m - 1;
-    float sc = 1.0f;
-    if (a.priv_avg > 0.0f) {
-      const float n = (float)gridDim.x * (float)(unsigned)readlane_i((int)hits_l, r) / (float)flushes;
-      sc = 1.0f / fmaxf(1.0f, n / a.priv_avg);
-    }
+    const float sc = a.priv_sc[r];
     float* dst = a.C + (int64_t)r * a.pitch + wave * kCols;
     for (int cc = lane; cc < kCols; cc += kWave) {
       float* p = &sh.priv[r][wave * kCols + cc];
@@ -441,7 +439,7 @@ __global__ __launch_bounds__(NW * kWave, WAVES_PER_SIMD) void train_shared_neg_k
   const __amdgpu_buffer_rsrc_t rW = rows_rsrc(a.W), rC = rows_rsrc(a.C);
   int par = 0;
   int since_flush = 0;  // centers since the private rows were written back
-  unsigned dirty = 0, flushes = 0, hits_l = 0;  // private rows: this wave's dirty mask and flush statistics
+  unsigned dirty = 0;  // private rows: this wave's dirty mask
   if (a.priv_n > 0) {
     for (int k = threadIdx.x; k < kSnPriv<KB, NW> * NW * KB * kSnTile; k += blockDim.x) (&sh.priv[0][0])[k] = 0.f;
     __syncthreads();
@@ -525,7 +523,7 @@ __global__ __launch_bounds__(NW * kWave, WAVES_PER_SIMD) void train_shared_neg_k
       for (int b = 0; b < n_batch; ++b) {
         sn_center<KB, NW>(a, sh, rW, rC, wave, lane, t_done + b, nk, b, alpha, par, cnt, prof, dirty);
         if (a.priv_n > 0 && ++since_flush >= a.flush_every) {
-          sn_flush_private<KB, NW>(a, sh, wave, lane, dirty, flushes, hits_l);
+          sn_flush_private<KB, NW>(a, sh, wave, lane, dirty);
           since_flush = 0;
         }
       }
@@ -534,7 +532,7 @@ __global__ __launch_bounds__(NW * kWave, WAVES_PER_SIMD) void train_shared_neg_k
     if (threadIdx.x == 0) atomicAdd(a.words, (unsigned long long)len);
     cnt.sentences += 1;
   }
-  if (a.priv_n > 0) sn_flush_private<KB, NW>(a, sh, wave, lane, dirty, flushes, hits_l);
+  if (a.priv_n > 0) sn_flush_private<KB, NW>(a, sh, wave, lane, dirty);
 #ifdef W2V_SN_PROF
   prof.stamp(0);
   if (lane == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))

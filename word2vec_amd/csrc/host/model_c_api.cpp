@@ -1,5 +1,6 @@
 // C bridge over the Word2Vec class (include/w2v_model.h).
 #include <cstring>
+#include <limits>
 #include <sstream>
 #include <stdexcept>
 #include <string>
@@ -31,6 +32,12 @@ std::vector<std::vector<std::string>> parse(const char* text, int64_t len) {
     out.push_back(std::move(s));
   }
   return out;
+}
+
+bool bad_word(w2v_model* m, int64_t i) {
+  if (i >= 0 && i < (int64_t)m->w.vocab.size()) return false;
+  m->err = "word index " + std::to_string(i) + " outside the vocab [0, " + std::to_string(m->w.vocab.size()) + ")";
+  return true;
 }
 
 RMatrixXf* pick(w2v_model* m, int which) {
@@ -139,11 +146,21 @@ int w2v_model_init_weights(w2v_model* m) {
 }
 
 int64_t w2v_model_vocab_size(w2v_model* m) { return (int64_t)m->w.vocab.size(); }
-const char* w2v_model_word(w2v_model* m, int64_t i) { return m->w.vocab[(size_t)i]->text.c_str(); }
-int64_t w2v_model_word_count(w2v_model* m, int64_t i) { return (int64_t)m->w.vocab[(size_t)i]->count; }
-float w2v_model_sample_probability(w2v_model* m, int64_t i) { return m->w.vocab[(size_t)i]->sample_probability; }
-int64_t w2v_model_path_length(w2v_model* m, int64_t i) { return (int64_t)m->w.vocab[(size_t)i]->codes.size(); }
+// Out-of-range word indices: NULL / -1 / NaN / 1, with the message in last_error.
+const char* w2v_model_word(w2v_model* m, int64_t i) {
+  return bad_word(m, i) ? nullptr : m->w.vocab[(size_t)i]->text.c_str();
+}
+int64_t w2v_model_word_count(w2v_model* m, int64_t i) {
+  return bad_word(m, i) ? -1 : (int64_t)m->w.vocab[(size_t)i]->count;
+}
+float w2v_model_sample_probability(w2v_model* m, int64_t i) {
+  return bad_word(m, i) ? std::numeric_limits<float>::quiet_NaN() : m->w.vocab[(size_t)i]->sample_probability;
+}
+int64_t w2v_model_path_length(w2v_model* m, int64_t i) {
+  return bad_word(m, i) ? -1 : (int64_t)m->w.vocab[(size_t)i]->codes.size();
+}
 int w2v_model_path(w2v_model* m, int64_t i, uint8_t* codes, int32_t* points) {
+  if (bad_word(m, i)) return 1;
   const Word* w = m->w.vocab[(size_t)i];
   for (size_t k = 0; k < w->codes.size(); ++k) {
     codes[k] = (uint8_t)w->codes[k];
@@ -167,9 +184,17 @@ int w2v_model_get_matrix(w2v_model* m, int32_t which, float* out) {
   std::memcpy(out, M->data(), sizeof(float) * (size_t)M->size());
   return 0;
 }
-int w2v_model_set_matrix(w2v_model* m, int32_t which, const float* in, int64_t rows) {
+int w2v_model_set_matrix(w2v_model* m, int32_t which, const float* in, int64_t rows, int64_t cols) {
   RMatrixXf* M = pick(m, which);
-  if (!M) return 1;
+  if (!M) {
+    m->err = "bad matrix selector";
+    return 1;
+  }
+  if (rows < 0 || cols != m->w.word_dim || (rows > 0 && !in)) {
+    m->err = "set_matrix: expected rows >= 0 x word_dim (" + std::to_string(m->w.word_dim) + ") columns, got " +
+             std::to_string(rows) + " x " + std::to_string(cols);
+    return 1;
+  }
   M->resize((RMatrixXf::Index)rows, m->w.word_dim);
   std::memcpy(M->data(), in, sizeof(float) * (size_t)M->size());
   return 0;
@@ -178,12 +203,16 @@ int w2v_model_set_matrix(w2v_model* m, int32_t which, const float* in, int64_t r
 int w2v_model_train_sentence(w2v_model* m, const int32_t* ids, int64_t n, float alpha, int32_t cbow) {
   return guard(m, [&] {
     std::vector<Word*> s;
-    for (int64_t k = 0; k < n; ++k) s.push_back(m->w.vocab[(size_t)ids[k]]);
+    for (int64_t k = 0; k < n; ++k) {
+      if (ids[k] < 0 || (size_t)ids[k] >= m->w.vocab.size()) throw std::out_of_range("train_sentence: token id out of vocab");
+      s.push_back(m->w.vocab[(size_t)ids[k]]);
+    }
     if (cbow) m->w.train_sentence_cbow(s, alpha);
     else m->w.train_sentence_sg(s, alpha);
   });
 }
 int w2v_model_negative_sampling(w2v_model* m, int64_t word, float* x, float* grad, int32_t which, float alpha) {
+  if (bad_word(m, word)) return 1;
   return guard(m, [&] {
     RowVectorXf xv((w2v_dense::Index)m->w.word_dim), gv((w2v_dense::Index)m->w.word_dim);
     std::memcpy(xv.data(), x, sizeof(float) * (size_t)m->w.word_dim);
@@ -193,6 +222,7 @@ int w2v_model_negative_sampling(w2v_model* m, int64_t word, float* x, float* gra
   });
 }
 int w2v_model_hierarchical_softmax(w2v_model* m, int64_t word, float* x, float* grad, float alpha) {
+  if (bad_word(m, word)) return 1;
   return guard(m, [&] {
     RowVectorXf xv((w2v_dense::Index)m->w.word_dim), gv((w2v_dense::Index)m->w.word_dim);
     std::memcpy(xv.data(), x, sizeof(float) * (size_t)m->w.word_dim);

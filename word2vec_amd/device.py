@@ -169,6 +169,10 @@ class DeviceTrainer:
         self._chk(self.lib.w2v_dev_read_stats(self.h, C.byref(st)), "w2v_dev_read_stats")
         return st.as_dict()
 
+    def knobs(self) -> str:
+        """Experiment environment variables this handle read at creation ("" if none)."""
+        return self.lib.w2v_dev_knobs(self.h).decode()
+
     def reset_stats(self):
         self._chk(self.lib.w2v_dev_reset_stats(self.h), "w2v_dev_reset_stats")
 

@@ -50,7 +50,7 @@ def _load():
             "w2v_model_table": (C.c_int, [P, P]),
             "w2v_model_rows": (I64, [P, I32]),
             "w2v_model_get_matrix": (C.c_int, [P, I32, P]),
-            "w2v_model_set_matrix": (C.c_int, [P, I32, P, I64]),
+            "w2v_model_set_matrix": (C.c_int, [P, I32, P, I64, I64]),
             "w2v_model_train_sentence": (C.c_int, [P, P, I64, F, I32]),
             "w2v_model_negative_sampling": (C.c_int, [P, I64, P, P, I32, F]),
             "w2v_model_hierarchical_softmax": (C.c_int, [P, I64, P, P, F]),
@@ -186,7 +186,7 @@ class Word2Vec:
 
     def vocab(self):
         V = self.V
-        words = [self.L.w2v_model_word(self.h, i).decode() for i in range(V)]
+        words = [self.L.w2v_model_word(self.h, i).decode() for i in range(V)]  # indices in range: never NULL
         counts = np.array([self.L.w2v_model_word_count(self.h, i) for i in range(V)], np.int64)
         return words, counts
 
@@ -223,4 +223,6 @@ class Word2Vec:
 
     def set_matrix(self, which: int, m):
         m = np.ascontiguousarray(m, np.float32)
-        self.L.w2v_model_set_matrix(self.h, which, _p(m), m.shape[0])
+        if m.ndim != 2 or m.shape[1] != self.word_dim:
+            raise ValueError(f"set_matrix: expected (rows, {self.word_dim}), got {m.shape}")
+        self._chk(self.L.w2v_model_set_matrix(self.h, which, _p(m), m.shape[0], m.shape[1]), "set_matrix")
