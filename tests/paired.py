@@ -68,10 +68,12 @@ def gpu_cfg(o, mode, p):
     return device_config(o, mode, p["dim"], p["window"], p["iters"], p["table_size"], True, p["init_alpha"], 2.5e-6)
 
 
-def train_gpu_paired(name, mode, seed, sents, max_waves=0, stats=None):
-    """The GPU side: the parallel schedule (Philox, default update policy)
-    with at most `max_waves` wavefronts in flight (0 = all that fit), from the
-    oracle's start on its draws. Returns (words, evaluated matrix)."""
+def train_gpu_paired(name, mode, seed, sents, max_waves=0, stats=None, policy=None):
+    """The GPU side: the parallel schedule (Philox, default update policy;
+    `policy` overrides it: hot_rows, private_rows, flush_centers,
+    private_average, context_rows, context_flush) with at most `max_waves`
+    wavefronts in flight (0 = all that fit), from the oracle's start on its
+    draws. Returns (words, evaluated matrix)."""
     from tests.harness import device_from_oracle
     from word2vec_amd import _native as N
 
@@ -80,6 +82,15 @@ def train_gpu_paired(name, mode, seed, sents, max_waves=0, stats=None):
     d.set_rng(N.W2V_RNG_PHILOX, key)
     d.set_schedule(N.W2V_SCHED_PARALLEL)
     d.set_max_waves(max_waves)
+    pol = dict(policy or {})
+    if "hot_rows" in pol:
+        d.set_hot_rows(pol["hot_rows"])
+    if "private_rows" in pol:
+        d.set_private_rows(pol["private_rows"])
+    if "flush_centers" in pol or "private_average" in pol:
+        d.set_private_sync(pol.get("flush_centers", 0), pol.get("private_average", 8.0))
+    if "context_rows" in pol or "context_flush" in pol:
+        d.set_context_private(pol.get("context_rows", -1), pol.get("context_flush", 0))
     d.set_progress(0)
     n = orders.size // p["iters"]
     for e in range(p["iters"]):
