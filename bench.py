@@ -70,8 +70,11 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
     # update policy of the parallel schedule (include/w2v_dev.h); defaults = the library's
-    ap.add_argument("--hot-rows", type=int, default=1000,
-                    help="rows updated with atomics (-1 all, 0 none = plain Hogwild RMW, k = k most frequent)")
+    ap.add_argument("--hot-rows", type=int, default=-2,
+                    help="rows updated with atomics (-2 auto from the corpus statistics, -1 all, 0 none = plain "
+                         "Hogwild RMW, k = k most frequent)")
+    ap.add_argument("--hot-auto", type=float, nargs=2, default=[1.0, 1.0], metavar=("ROWS", "NODES"),
+                    help="thresholds of the automatic hot rows (expected updates in flight of a W / C row, a node)")
     ap.add_argument("--private-rows", type=int, default=-1,
                     help="hottest output rows privatised per workgroup in LDS (-1 auto, 0 off)")
     ap.add_argument("--flush-centers", type=int, default=0,
@@ -208,6 +211,7 @@ def main():
         tr.set_update(N.W2V_UPDATE_SHARED_NEGATIVES)
     tr.set_schedule(N.W2V_SCHED_PARALLEL)
     tr.set_hot_rows(args.hot_rows)
+    tr.set_hot_auto(*args.hot_auto)
     tr.set_private_rows(args.private_rows)
     tr.set_private_sync(args.flush_centers, args.private_average)
     tr.set_max_waves(args.max_waves)
@@ -330,6 +334,8 @@ def main():
                 "context_flush": args.context_flush,
                 "kept_centers_per_step": int(delta["centers"] / args.steps),
                 "env_knobs": tr.knobs(),
+                "hot_auto": args.hot_auto,
+                "policy_used": tr.policy(),
                 "targets_per_step": int(delta["targets"] / args.steps),
             },
             "roofline": roofline,

@@ -98,7 +98,7 @@ class Word2Vec {
                              // wavefront (deterministic, equals the reference run
                              // single-threaded up to fp32 summation order)
   // parallel-schedule update policy (include/w2v_dev.h, w2v_dev_set_hot_rows ff.)
-  int64_t hot_rows = 1000;      // rows updated with device atomics: -1 all, 0 none
+  int64_t hot_rows = W2V_HOT_AUTO;  // rows updated with device atomics: -2 auto (from the corpus), -1 all, 0 none
   int private_rows = -1;        // hottest output rows privatised in LDS: -1 as many as fit, 0 off
   int flush_centers = 0;        // workgroup centers between private-row flushes (0 = auto)
   float private_average = 8.f;  // concurrency the private rows' summed deltas are scaled to (0 = sum)

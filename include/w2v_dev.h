@@ -178,13 +178,24 @@ int w2v_dev_reset_stats(w2v_dev* h);
  *    0 = off;
  *  - hot rows: rows of W and C with index < hot_rows, and the hot_rows internal
  *    Huffman nodes nearest the root, take memory-side float atomic adds: no
- *    update is lost however many wavefronts hit the row. -1 = every row,
- *    0 = none; default 1000;
+ *    update is lost however many wavefronts hit the row. W2V_HOT_AUTO (-2,
+ *    the default) = chosen per launch from the corpus statistics: the rows
+ *    and nodes whose expected updates in flight (wavefronts x expected
+ *    updates per center) reach the thresholds of w2v_dev_set_hot_auto
+ *    (default 1 for both); -1 = every row, 0 = none,
+ *    k > 0 = the k most frequent;
  *  - the rest: plain read-modify-write (an update racing another on the same
  *    row can be lost, as between the reference's threads).
  * Same fp32 rounding per update in every class. None of this applies to the
  * sequential schedule (W2V_SCHED_SEQUENTIAL), which is reference-exact. */
+#define W2V_HOT_AUTO (-2)
 int w2v_dev_set_hot_rows(w2v_dev* h, int64_t hot_rows);
+/* Thresholds of the automatic hot rows: expected updates of a W / C row, of
+ * a Huffman node, in flight across the chip (> 0; defaults 1 and 1). */
+int w2v_dev_set_hot_auto(w2v_dev* h, float tau_rows, float tau_nodes);
+/* The update policy the last parallel launch used: hot W / C rows, hot
+ * Huffman nodes, LDS-private output rows, LDS-private context rows. */
+int w2v_dev_policy(w2v_dev* h, int64_t* hot_rows, int64_t* hot_nodes, int32_t* private_rows, int32_t* context_rows);
 int w2v_dev_set_private_rows(w2v_dev* h, int32_t n);
 /* flush_centers: workgroup centers between flushes (0 = auto: 1024 for NS, 64
  * for HS); average_over: the concurrency a private row's summed deltas are

@@ -26,6 +26,7 @@ W2V_SCHED_PARALLEL = 0
 W2V_SCHED_SEQUENTIAL = 1
 W2V_UPDATE_PER_PAIR = 0
 W2V_UPDATE_SHARED_NEGATIVES = 1
+W2V_HOT_AUTO = -2
 
 
 class DevConfig(C.Structure):
@@ -94,6 +95,8 @@ SIGNATURES = {
     "w2v_dev_reset_stats": (C.c_int, [_P]),
     "w2v_dev_set_fixed_alpha": (C.c_int, [_P, _F]),
     "w2v_dev_set_hot_rows": (C.c_int, [_P, _I64]),
+    "w2v_dev_set_hot_auto": (C.c_int, [_P, _F, _F]),
+    "w2v_dev_policy": (C.c_int, [_P, C.POINTER(_I64), C.POINTER(_I64), C.POINTER(_I32), C.POINTER(_I32)]),
     "w2v_dev_set_private_rows": (C.c_int, [_P, _I32]),
     "w2v_dev_set_private_sync": (C.c_int, [_P, _I32, _F]),
     "w2v_dev_set_context_private": (C.c_int, [_P, _I32, _I32]),

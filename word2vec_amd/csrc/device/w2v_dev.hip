@@ -10,6 +10,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "w2v_dev.h"
@@ -106,7 +107,7 @@ struct w2v_dev {
   int64_t pitch = 0;
   int32_t d4 = 0;
   int nv = 1;                 // floats per lane per row (instantiated width >= ceil(d / 64))
-  int64_t hot_rows = 1000;    // rows updated with atomics: -1 = all, 0 = none
+  int64_t hot_rows = W2V_HOT_AUTO;  // rows updated with atomics: -2 = auto, -1 = all, 0 = none
   int32_t private_rows = -1;  // hottest output rows privatised in LDS: -1 = auto, 0 = off
   int32_t flush_centers = 0;  // workgroup centers between flushes of the privatised rows (0 = auto)
   float private_average = 8.0f;  // concurrency the privatised rows' summed deltas are scaled to (0 = plain sum)
@@ -144,13 +145,65 @@ struct w2v_dev {
   int n_cu = 256;
   bool model_ready = false, vocab_ready = false, corpus_ready = false;
   bool model_bound = false;  // W/C/S owned by the caller
-  // Host statistics for the privatised rows' flush scales (priv_scales):
+  // Host statistics of the vocab and corpus, for the update policy's
+  // frequency-derived settings (row_stats: flush scales, automatic hot rows):
   std::vector<float> keep_h;        // sample probabilities
-  std::vector<double> table_frac;   // unigram-table share of rows [0, kPrivMax)
-  std::vector<int32_t> top_node;    // HS: per word, the deepest node of its path among the kPrivMax nearest the root (-1: none)
-  std::vector<int32_t> node_parent; // HS: parent of node (V - 1 - kPrivMax + j), -1 for the root
+  std::vector<double> table_frac;   // unigram-table share of each word
+  std::vector<int32_t> leaf_node;   // HS: per word, the deepest internal node of its path (-1: none)
+  std::vector<int32_t> node_parent; // HS: parent of each internal node, -1 for the root
   std::vector<int64_t> tok_count;   // corpus token count per word
+  uint64_t data_version = 0;        // bumped by every upload that changes the statistics
+  // derived (row_stats): per word f = token share, fk = kept-center share;
+  // per internal node the same summed over the words below it
+  uint64_t stats_version = ~0ull;
+  bool stats_ok = false;
+  std::vector<double> f, fk, node_f, node_fk;
+  double hot_tau_rows = 1.0;        // automatic hot rows: expected concurrent updates threshold, W / C rows
+  double hot_tau_nodes = 1.0;       //   ... and Huffman nodes
+  // the policy the last parallel launch used (w2v_dev_policy)
+  int64_t last_hot_rows = 0, last_hot_nodes = 0;
+  int32_t last_priv = 0, last_ctx = 0;
 };
+
+// Per-word and per-node shares of the corpus (cached until the next upload).
+static void row_stats(w2v_dev* h) {
+  if (h->stats_version == h->data_version) return;
+  h->stats_version = h->data_version;
+  const int64_t V = h->V;
+  h->stats_ok = V > 0 && (int64_t)h->tok_count.size() == V && (int64_t)h->keep_h.size() == V;
+  h->f.assign((size_t)std::max<int64_t>(V, 0), 0.0);
+  h->fk.assign(h->f.size(), 0.0);
+  h->node_f.clear();
+  h->node_fk.clear();
+  if (!h->stats_ok) return;
+  double N = 0.0, K = 0.0;
+  for (int64_t w = 0; w < V; ++w) {
+    N += (double)h->tok_count[(size_t)w];
+    K += (double)h->tok_count[(size_t)w] * std::min(1.0, (double)h->keep_h[(size_t)w]);
+  }
+  if (!(N > 0.0 && K > 0.0)) {
+    h->stats_ok = false;
+    return;
+  }
+  for (int64_t w = 0; w < V; ++w) {
+    h->f[(size_t)w] = (double)h->tok_count[(size_t)w] / N;
+    h->fk[(size_t)w] = (double)h->tok_count[(size_t)w] * std::min(1.0, (double)h->keep_h[(size_t)w]) / K;
+  }
+  if ((int64_t)h->leaf_node.size() == V && (int64_t)h->node_parent.size() == V - 1) {
+    h->node_f.assign((size_t)(V - 1), 0.0);
+    h->node_fk.assign((size_t)(V - 1), 0.0);
+    for (int64_t w = 0; w < V; ++w)
+      if (h->leaf_node[(size_t)w] >= 0) {
+        h->node_f[(size_t)h->leaf_node[(size_t)w]] += h->f[(size_t)w];
+        h->node_fk[(size_t)h->leaf_node[(size_t)w]] += h->fk[(size_t)w];
+      }
+    for (int64_t j = 0; j < V - 1; ++j)  // a node is created after its children: ids ascend towards the root
+      if (h->node_parent[(size_t)j] >= 0) {
+        h->node_f[(size_t)h->node_parent[(size_t)j]] += h->node_f[(size_t)j];
+        h->node_fk[(size_t)h->node_parent[(size_t)j]] += h->node_fk[(size_t)j];
+      }
+  }
+}
 
 namespace {
 
@@ -369,31 +422,30 @@ int w2v_dev_upload_vocab(w2v_dev* h, int64_t V, const float* keep, const int64_t
     h->tok_count.clear();  // the corpus statistics refer to the old ids
   }
   h->V = V;
+  ++h->data_version;
   dfree(h->keep);
   h->keep = dkeep;
   h->keep_h.assign(keep, keep + V);
   if (dtable) {
     dfree(h->table);
     h->table = dtable;
-    h->table_frac.assign((size_t)std::min<int64_t>(V, w2v::kPrivMax), 0.0);
+    h->table_frac.assign((size_t)V, 0.0);
     for (size_t r = 0; r < h->table_frac.size(); ++r) h->table_frac[r] = (double)(bounds[r + 1] - bounds[r]) / (double)n;
   }
   if (h->cfg.hs) {
     dfree(h->codes); dfree(h->points); dfree(h->coff);
     h->codes = dcodes; h->points = dpoints; h->coff = dcoff;
     h->n_codes = nc;
-    // the kPrivMax internal nodes nearest the root (ids V-1-kPrivMax .. V-2;
-    // a node is created after its children, so the range is closed upwards)
-    const int64_t lo = std::max<int64_t>(0, V - 1 - w2v::kPrivMax);
-    h->top_node.assign((size_t)V, -1);
-    h->node_parent.assign((size_t)(V - 1 - lo), -1);
+    // the tree's shape, for the per-node statistics: paths run root -> leaf
+    h->leaf_node.assign((size_t)V, -1);
+    h->node_parent.assign((size_t)(V - 1), -1);
     for (int64_t w = 0; w < V; ++w) {
       int32_t prev = -1;
-      for (int64_t t = coff[w]; t < coff[w + 1] && points[t] >= lo; ++t) {  // paths run root -> leaf
-        h->node_parent[(size_t)(points[t] - lo)] = prev;
+      for (int64_t t = coff[w]; t < coff[w + 1]; ++t) {
+        h->node_parent[(size_t)points[t]] = prev;
         prev = points[t];
       }
-      h->top_node[(size_t)w] = prev;
+      h->leaf_node[(size_t)w] = prev;
     }
   }
   h->vocab_ready = true;
@@ -407,9 +459,10 @@ int w2v_dev_upload_table(w2v_dev* h, const uint32_t* table, int64_t n) {
   dfree(h->table);
   HIP_TRY(hipMalloc(&h->table, n * sizeof(uint32_t)));
   HIP_TRY(hipMemcpy(h->table, table, n * sizeof(uint32_t), hipMemcpyHostToDevice));
-  h->table_frac.assign(w2v::kPrivMax, 0.0);
+  h->table_frac.assign((size_t)std::max<int64_t>(h->V, 0), 0.0);
   for (int64_t i = 0; i < n; ++i)
-    if (table[i] < (uint32_t)w2v::kPrivMax) h->table_frac[table[i]] += 1.0 / (double)n;
+    if ((int64_t)table[i] < h->V) h->table_frac[table[i]] += 1.0 / (double)n;
+  ++h->data_version;
   return W2V_OK;
 }
 
@@ -526,6 +579,7 @@ int w2v_dev_upload_corpus(w2v_dev* h, const int32_t* ids, int64_t n_tok, const i
   h->max_len = max_len;
   h->train_words = train_words;
   h->tok_count.swap(hist);
+  ++h->data_version;
   h->corpus_ready = true;
   return W2V_OK;
 }
@@ -583,43 +637,29 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
 //   SG-HS nodes            (window + 1) sum_{w below} f(w)   every context's path (:342-345)
 //   CBOW-HS nodes          sum_{w below} fk(w)               the center's path (:304-306)
 //   CBOW context (C) rows  (window + 1) f(r)                 window positions (:288-300)
-static void priv_scales(const w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool shared) {
+static void priv_scales(w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool shared) {
   for (int p = 0; p < w2v::kPrivMax; ++p) a.priv_sc[p] = 1.0f;
   for (int p = 0; p < w2v::kCtxMax; ++p) a.ctx_sc[p] = 1.0f;
   if (!(a.priv_avg > 0.0f) || (a.priv_n == 0 && a.ctx_n == 0)) return;
+  row_stats(h);
   const double S = a.priv_avg, win1 = (double)h->cfg.window + 1.0, neg = (double)h->cfg.negative;
   const int64_t V = h->V;
-  double N = 0.0, K = 0.0;
-  const bool have = (int64_t)h->tok_count.size() == V && (int64_t)h->keep_h.size() == V;
-  if (have)
-    for (int64_t w = 0; w < V; ++w) {
-      N += (double)h->tok_count[(size_t)w];
-      K += (double)h->tok_count[(size_t)w] * std::min(1.0, (double)h->keep_h[(size_t)w]);
-    }
-  auto sc = [&](double m, int k) {
-    const double n = (N > 0.0 && K > 0.0) ? (double)G * (1.0 - std::exp(-(double)k * m)) : (double)G;
+  const bool ok = h->stats_ok;
+  auto sc = [&](double m, int k) {  // without statistics: every workgroup counted (the most damping)
+    const double n = ok ? (double)G * (1.0 - std::exp(-(double)k * m)) : (double)G;
     return (float)(1.0 / std::max(1.0, n / S));
   };
-  auto f = [&](int64_t r) { return N > 0.0 ? (double)h->tok_count[(size_t)r] / N : 0.0; };
-  auto fk = [&](int64_t r) {
-    return K > 0.0 ? (double)h->tok_count[(size_t)r] * std::min(1.0, (double)h->keep_h[(size_t)r]) / K : 0.0;
-  };
+  auto f = [&](int64_t r) { return ok ? h->f[(size_t)r] : 0.0; };
+  auto fk = [&](int64_t r) { return ok ? h->fk[(size_t)r] : 0.0; };
   auto u = [&](int64_t r) { return r < (int64_t)h->table_frac.size() ? h->table_frac[(size_t)r] : 0.0; };
   const bool cbow = h->cfg.cbow != 0;
   if (a.priv_n > 0) {
     if (!shared && h->cfg.hs) {
-      const int64_t lo = std::max<int64_t>(0, V - 1 - w2v::kPrivMax);
-      std::vector<double> acc(h->node_parent.size(), 0.0);
-      if (have && h->top_node.size() == (size_t)V) {
-        for (int64_t w = 0; w < V; ++w)
-          if (h->top_node[(size_t)w] >= 0) acc[(size_t)(h->top_node[(size_t)w] - lo)] += cbow ? fk(w) : f(w);
-        for (size_t j = 0; j < acc.size(); ++j)  // children have lower ids than their parents
-          if (h->node_parent[j] >= 0) acc[(size_t)(h->node_parent[j] - lo)] += acc[j];
-      }
+      const bool nodes = ok && (int64_t)h->node_f.size() == V - 1;
       for (int p = 0; p < a.priv_n; ++p) {
-        const int64_t j = a.priv_lo + p - lo;
-        const double m = (j >= 0 && j < (int64_t)acc.size()) ? acc[(size_t)j] : 1.0;
-        a.priv_sc[p] = sc(cbow ? m : win1 * m, a.flush_every);
+        const int64_t j = a.priv_lo + p;
+        const double m = !nodes ? 1.0 : cbow ? h->node_fk[(size_t)j] : win1 * h->node_f[(size_t)j];
+        a.priv_sc[p] = sc(m, a.flush_every);
       }
     } else {
       for (int p = 0; p < a.priv_n; ++p) {
@@ -630,6 +670,45 @@ static void priv_scales(const w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool sha
     }
   }
   for (int p = 0; p < a.ctx_n; ++p) a.ctx_sc[p] = sc(win1 * f(p), a.ctx_flush_every);
+}
+
+// Automatic hot rows (hot_rows == W2V_HOT_AUTO): the rows (and Huffman nodes)
+// whose expected number of updates in flight across the chip, waves x their
+// expected updates per center, is at least hot_tau. A row that several
+// wavefronts update at once loses updates under plain read-modify-write and
+// is read stale across the non-coherent XCD L2s, so those rows take
+// memory-side atomics. Measured on the text8-like CBOW-HS workload (DESIGN.md
+// §4.1): a fixed 1000 rows cut through the planted words' Huffman nodes
+// (analogy 19.8 vs the oracle's 21.4); 2000 / 4000 / 16000 rows: 36.7 /
+// 43.3 / 43.0; this rule at threshold 0.5 / 1 / 2: 42.9 / 43.7 / 44.4. At
+// threshold 4 for the W / C rows the planted SG-HS run collapses (analogy
+// 6 vs 89: its center rows, V = 3.4K under 8K waves, fell to plain
+// read-modify-write; profiles/r02c_*). Returns {W / C rows, nodes}.
+static std::pair<int64_t, int64_t> auto_hot(w2v_dev* h, double waves, bool shared) {
+  row_stats(h);
+  const int64_t V = h->V;
+  if (!h->stats_ok) return {std::min<int64_t>(V, 1000), std::min<int64_t>(std::max<int64_t>(V - 1, 0), 1000)};
+  const double win1 = (double)h->cfg.window + 1.0, tau = h->hot_tau_rows;
+  const bool cbow = h->cfg.cbow != 0, ns = h->cfg.negative > 0;
+  int64_t rows = 0;
+  for (int64_t r = 0; r < V; ++r) {  // largest rate over the row's roles in W and C
+    // Positive-label updates only: an NS output row's negative-sample updates
+    // (label 0, sigma(f) small for most draws) are small. Counting them put
+    // 13K rows (c3) in the atomic class where these give 2.3K, for the same
+    // paired scores and 2.5 % less throughput (profiles/r02b_*, r02c_*).
+    double m;
+    if (shared) m = std::max(win1 * h->fk[(size_t)r], h->fk[(size_t)r]);   // W: window inputs; C: the center
+    else if (cbow) m = std::max(win1 * h->f[(size_t)r], ns ? h->fk[(size_t)r] : 0.0);  // C: contexts; W: center
+    else m = std::max(h->fk[(size_t)r], ns ? win1 * h->f[(size_t)r] : 0.0);            // W: center; C: contexts
+    if (waves * m >= tau) rows = r + 1;
+  }
+  int64_t nodes = 0;
+  if (h->cfg.hs && (int64_t)h->node_f.size() == V - 1)
+    for (int64_t j = 0; j < V - 1; ++j) {
+      const double m = cbow ? h->node_fk[(size_t)j] : win1 * h->node_f[(size_t)j];
+      if (waves * m >= h->hot_tau_nodes) ++nodes;
+    }
+  return {std::max<int64_t>(rows, std::min<int64_t>(V, 64)), nodes};
 }
 
 // The shared-negatives minibatch covers skip-gram NS only: a 16 x 16 MFMA tile
@@ -695,11 +774,14 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   a.key0 = (uint32_t)h->seed; a.key1 = (uint32_t)(h->seed >> 32);
   a.epoch = (uint32_t)epoch;
   a.fixed_alpha = h->fixed_alpha;
-  {
-    const int64_t hot = h->hot_rows < 0 ? h->V : (h->hot_rows < h->V ? h->hot_rows : h->V);
-    a.hot_wc = hot;
-    a.hot_s = (h->V - 1) - hot;  // the top `hot` internal nodes (the root is V-2)
-  }
+  // Hot rows (memory-side atomic updates) for `waves` updaters in flight:
+  // {W / C rows [0, rows), the `nodes` internal nodes nearest the root}.
+  auto hot_for = [&](double waves, bool shared) -> std::pair<int64_t, int64_t> {
+    const int64_t V = h->V, nV = std::max<int64_t>(V - 1, 0);
+    if (h->hot_rows == W2V_HOT_AUTO) return auto_hot(h, waves, shared);
+    if (h->hot_rows < 0) return {V, nV};
+    return {std::min<int64_t>(h->hot_rows, V), std::min<int64_t>(h->hot_rows, nV)};
+  };
   a.strict = h->sched == W2V_SCHED_SEQUENTIAL ? 1 : 0;
   // Workgroup shape: up to 16 waves share the LDS-privatised rows (kMaxBlock);
   // under a wave cap, narrower workgroups so the capped grid still spans the CUs.
@@ -790,12 +872,6 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     // device-coherent rows (rows_rsrc in w2v_shared.hpp): all for hot_rows =
     // -1, else at least the rows two XCD L2s' capacity could keep resident
     const int64_t l2_rows = (int64_t)(8 << 20) / (h->pitch * (int64_t)sizeof(float));
-    a.hot_wc = h->hot_rows < 0 ? h->V : std::min<int64_t>(h->V, std::max<int64_t>(h->hot_rows, l2_rows));
-    if (h->knobs.sn_coherent_rows >= 0) a.hot_wc = std::min<int64_t>(h->V, h->knobs.sn_coherent_rows);  // experiments
-    // the hot_rows most frequent rows take atomic deltas, as in the per-pair
-    // kernel (parallel schedule only: the sequential one is exact either way)
-    a.hot_atomic = h->sched == W2V_SCHED_PARALLEL ? std::min<int64_t>(h->V, h->hot_rows < 0 ? h->V : h->hot_rows) : 0;
-    if (h->knobs.sn_atomic_rows >= 0) a.hot_atomic = std::min<int64_t>(h->V, h->knobs.sn_atomic_rows);  // experiments
     int64_t g = 1;
     if (h->sched == W2V_SCHED_PARALLEL) {
       int per_cu = 0;
@@ -809,7 +885,20 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
       g = std::min<int64_t>((int64_t)per_cu * h->n_cu, count);
       if (h->max_waves > 0) g = std::max<int64_t>(1, std::min<int64_t>(g, h->max_waves / sn_waves));
     }
+    // the hot rows (one updater per workgroup) take atomic deltas, as in the
+    // per-pair kernel (parallel schedule only: the sequential one is exact
+    // either way), and at least the rows two XCD L2s could keep resident are
+    // device-coherent
+    const int64_t hot = hot_for((double)g, true).first;
+    a.hot_wc = h->hot_rows == -1 ? h->V : std::min<int64_t>(h->V, std::max<int64_t>(hot, l2_rows));
+    if (h->knobs.sn_coherent_rows >= 0) a.hot_wc = std::min<int64_t>(h->V, h->knobs.sn_coherent_rows);  // experiments
+    a.hot_atomic = h->sched == W2V_SCHED_PARALLEL ? hot : 0;
+    if (h->knobs.sn_atomic_rows >= 0) a.hot_atomic = std::min<int64_t>(h->V, h->knobs.sn_atomic_rows);  // experiments
     priv_scales(h, a, g, true);
+    h->last_hot_rows = a.hot_atomic;
+    h->last_hot_nodes = 0;
+    h->last_priv = a.priv_n;
+    h->last_ctx = 0;
     HIP_TRY(hipMemsetAsync(h->work, 0, sizeof(unsigned int), h->stream));
     hipLaunchKernelGGL(sn_fn, dim3((unsigned)g), dim3(threads), 0, h->stream, a);
     HIP_TRY(hipGetLastError());
@@ -830,6 +919,15 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     if (h->knobs.max_blocks > 0 && h->knobs.max_blocks < g) g = h->knobs.max_blocks;  // diagnostics only
     grid = dim3((unsigned)g);
     block = dim3(threads);
+  }
+  {
+    const std::pair<int64_t, int64_t> hot = hot_for((double)grid.x * (block.x / w2v::kWave), false);
+    a.hot_wc = hot.first;
+    a.hot_s = (h->V - 1) - hot.second;  // the `nodes` internal nodes nearest the root (the root is V-2)
+    h->last_hot_rows = hot.first;
+    h->last_hot_nodes = h->cfg.hs ? hot.second : 0;
+    h->last_priv = a.priv_n;
+    h->last_ctx = a.ctx_n;
   }
   // Sentence segments as work items (parallel Philox schedule): the launch's
   // last round shrinks from a whole sentence per wave to one segment. With
@@ -977,8 +1075,25 @@ int w2v_dev_set_update(w2v_dev* h, int32_t mode) {
 
 int w2v_dev_set_hot_rows(w2v_dev* h, int64_t hot_rows) {
   if (!h) return fail(W2V_ERR_ARG, "null handle");
-  if (hot_rows < -1) return fail(W2V_ERR_ARG, "hot_rows must be >= -1");
+  if (hot_rows < W2V_HOT_AUTO) return fail(W2V_ERR_ARG, "hot_rows must be >= -2 (W2V_HOT_AUTO)");
   h->hot_rows = hot_rows;
+  return W2V_OK;
+}
+
+int w2v_dev_set_hot_auto(w2v_dev* h, float tau_rows, float tau_nodes) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (!(tau_rows > 0.0f) || !(tau_nodes > 0.0f)) return fail(W2V_ERR_ARG, "the automatic hot-row thresholds must be > 0");
+  h->hot_tau_rows = tau_rows;
+  h->hot_tau_nodes = tau_nodes;
+  return W2V_OK;
+}
+
+int w2v_dev_policy(w2v_dev* h, int64_t* hot_rows, int64_t* hot_nodes, int32_t* private_rows, int32_t* context_rows) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (hot_rows) *hot_rows = h->last_hot_rows;
+  if (hot_nodes) *hot_nodes = h->last_hot_nodes;
+  if (private_rows) *private_rows = h->last_priv;
+  if (context_rows) *context_rows = h->last_ctx;
   return W2V_OK;
 }
 

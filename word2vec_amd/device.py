@@ -177,8 +177,19 @@ class DeviceTrainer:
         self._chk(self.lib.w2v_dev_reset_stats(self.h), "w2v_dev_reset_stats")
 
     def set_hot_rows(self, hot_rows: int):
-        """Rows updated with atomics: -1 = all, 0 = none (plain Hogwild RMW), k = the k most frequent (default 1000)."""
+        """Rows updated with atomics: -2 = auto from the corpus statistics (default), -1 = all,
+        0 = none (plain Hogwild RMW), k = the k most frequent."""
         self._chk(self.lib.w2v_dev_set_hot_rows(self.h, int(hot_rows)), "w2v_dev_set_hot_rows")
+
+    def set_hot_auto(self, tau_rows: float = 1.0, tau_nodes: float = 1.0):
+        """Thresholds of the automatic hot rows (expected updates in flight of a W / C row, of a Huffman node)."""
+        self._chk(self.lib.w2v_dev_set_hot_auto(self.h, float(tau_rows), float(tau_nodes)), "w2v_dev_set_hot_auto")
+
+    def policy(self) -> dict:
+        """The update policy the last parallel launch used."""
+        r, n, p, c = C.c_int64(), C.c_int64(), C.c_int32(), C.c_int32()
+        self._chk(self.lib.w2v_dev_policy(self.h, C.byref(r), C.byref(n), C.byref(p), C.byref(c)), "w2v_dev_policy")
+        return {"hot_rows": r.value, "hot_nodes": n.value, "private_rows": p.value, "context_rows": c.value}
 
     def set_private_rows(self, n: int):
         """Hottest output rows privatised per workgroup in LDS: -1 auto (default), 0 off."""

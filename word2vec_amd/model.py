@@ -81,7 +81,7 @@ class Word2Vec:
 
     def __init__(self, iter=1, window=5, min_count=5, table_size=100_000_000, word_dim=200, negative=0,
                  subsample_threshold=0.001, init_alpha=0.025, min_alpha=1e-6, cbow_mean=False, num_threads=1,
-                 train_method="hs", model="cbow", gpu_device=0, replay_rng=False, verbose=False, hot_rows=1000,
+                 train_method="hs", model="cbow", gpu_device=0, replay_rng=False, verbose=False, hot_rows=-2,
                  private_rows=-1, flush_centers=0, private_average=8.0, max_waves=0, shared_negatives=False,
                  context_rows=-1, context_flush=0):
         self.L = _load()
