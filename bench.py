@@ -7,8 +7,9 @@ synthetic Zipf(s=1) corpus over 1M word ranks in 1000-token sentences (the
 1B-Word corpus is not available offline). One "step" = one training pass
 (epoch) of the hot path over this rank's shard, inputs already resident in HBM.
 With N GPUs (torchrun), every rank trains its own shard of the same size on a
-full model replica and the replicas are averaged with an RCCL all-reduce after
-every step (weak scaling).
+full model replica and the replicas are averaged by the library's RCCL group
+(include/w2v_dev.h w2v_group_*, overlapped with the next round) after every
+step (weak scaling); torch.distributed (gloo) carries only control messages.
 
 Prints ONE JSON line on rank 0 (metric/value/unit/... + roofline + cpu_baseline).
 """
@@ -77,6 +78,8 @@ def parse():
                     help="thresholds of the automatic hot rows (expected updates in flight of a W / C row, a node)")
     ap.add_argument("--private-rows", type=int, default=-1,
                     help="hottest output rows privatised per workgroup in LDS (-1 auto, 0 off)")
+    ap.add_argument("--private-rate", type=float, default=None,
+                    help="privatise only rows updated >= this many times per center (default: the library's)")
     ap.add_argument("--flush-centers", type=int, default=0,
                     help="workgroup centers between private-row flushes (0 = auto)")
     ap.add_argument("--private-average", type=float, default=8.0,
@@ -89,6 +92,9 @@ def parse():
                     help="N=1 only: let the library allocate the matrices instead of torch")
     ap.add_argument("--sync-every", type=int, default=0,
                     help="average the replicas every this many sentences of a shard (0 = once per step)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N>1: average the replicas in place on the training stream instead of from a snapshot "
+                         "on a communication stream overlapped with the next round")
     args = ap.parse_args()
     if args.config:
         for k, v in CONFIGS[args.config].items():
@@ -117,15 +123,15 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        if share:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=dev)
+        # control plane only (vocab counts, the group id, barriers, max time):
+        # the replicas are averaged by the library's own RCCL group
+        dist.init_process_group("gloo")
 
     from word2vec_amd import _native as N
     from word2vec_amd import host
     from word2vec_amd.device import Config, DeviceTrainer
-    from word2vec_amd.replicas import ReplicaGroup, n_rounds, train_rounds
+    from word2vec_amd.replicas import (NativeAverager, TorchAverager, global_round_words, group_unique_id,
+                                       local_round_words, n_rounds, train_rounds)
 
     mode = MODES[args.mode]
     neg = 0 if mode["hs"] else args.negative
@@ -148,8 +154,10 @@ def main():
         ranks[s:e] = torch.searchsorted(cdf, u, right=True).clamp_(max=args.vocab - 1)
         del u
     counts = torch.bincount(ranks, minlength=args.vocab)
-    if world > 1:
-        dist.all_reduce(counts)  # one vocab for all replicas (built over the whole corpus)
+    if world > 1:  # one vocab for all replicas (built over the whole corpus)
+        cc = counts.cpu()
+        dist.all_reduce(cc)
+        counts = cc.to(dev)
     order = torch.argsort(counts, descending=True, stable=True)
     V = int((counts >= args.min_count).sum())
     vocab_ranks = order[:V]
@@ -205,7 +213,9 @@ def main():
     else:
         tr.bind_model(W.data_ptr(), Cm.data_ptr() if Cm is not None else None,
                       S.data_ptr() if S is not None else None, pitch)
-    tr.upload_corpus(ids_h, soff_h, n_tok * world)  # alpha follows the global raw-token total
+    # alpha follows the global schedule: train_words = (global raw tokens) / world
+    # with each round's counter at (global words) / world (replicas.train_rounds)
+    tr.upload_corpus(ids_h, soff_h, n_tok)
     tr.set_rng(N.W2V_RNG_PHILOX, (args.seed << 32) | (rank + 1))
     if mode.get("shared"):
         tr.set_update(N.W2V_UPDATE_SHARED_NEGATIVES)
@@ -213,6 +223,8 @@ def main():
     tr.set_hot_rows(args.hot_rows)
     tr.set_hot_auto(*args.hot_auto)
     tr.set_private_rows(args.private_rows)
+    if args.private_rate is not None:
+        tr.set_private_rate(args.private_rate)
     tr.set_private_sync(args.flush_centers, args.private_average)
     tr.set_max_waves(args.max_waves)
     tr.set_context_private(args.context_rows, args.context_flush)
@@ -223,17 +235,24 @@ def main():
     mats = [m for m in (W, Cm, S) if m is not None]
     if not mats:
         assert world == 1
-    replicas = ReplicaGroup(mats, world)
+    if world > 1 and not share:
+        uid = [group_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        averager = NativeAverager([tr], uid[0], world, rank, overlap=not args.no_overlap)
+    else:  # N = 1 (no-op) or the one-GPU rehearsal (ranks share cuda:0: RCCL needs one rank per GPU)
+        averager = TorchAverager(mats, world)
     rounds = n_rounds(n_sent * world, world, args.sync_every)
     order_dev = torch.arange(n_sent, dtype=torch.int64, device=dev)  # this rank's shard, in order
+    round_words = global_round_words(local_round_words(soff_h, range(n_sent), rounds), world)
     progress = 0
 
     def step(epoch, evs=None):
         nonlocal progress
-        progress = train_rounds(tr, replicas, order_dev, epoch, rounds, dev, progress, evs)
+        progress = train_rounds(tr, averager, order_dev, epoch, rounds, progress, round_words, world, evs)
 
     for w in range(args.warmup):
         step(w)
+    averager.finish()
     torch.cuda.synchronize()
     st0 = tr.read_stats()
     events = []
@@ -243,6 +262,7 @@ def main():
     t_start = time.perf_counter()
     for k in range(args.steps):
         step(args.warmup + k, events)
+    averager.finish()  # the last (overlapped) average is folded in inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -255,10 +275,10 @@ def main():
     assert delta["sentences"] == n_sent * args.steps, delta
     words_local = int(ids_h.size) * args.steps
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        wsum = torch.tensor([words_local], dtype=torch.int64, device=dev)
+        wsum = torch.tensor([words_local], dtype=torch.int64)
         dist.all_reduce(wsum)
         words_total = int(wsum.item())
     else:
@@ -324,7 +344,8 @@ def main():
                 "vocab_size": V,
                 "global_batch": n_tok * world,
                 "parallelism": (f"dp{world}: full replica per GPU, corpus shard per GPU, RCCL all-reduce "
-                                f"average x{rounds} per step" if world > 1 else "dp1"),
+                                f"average (w2v_group, {'overlapped' if not args.no_overlap else 'blocking'}) "
+                                f"x{rounds} per step" if world > 1 else "dp1"),
                 "hot_rows": args.hot_rows,
                 "private_rows": args.private_rows,
                 "flush_centers": args.flush_centers,
@@ -344,6 +365,8 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if isinstance(averager, NativeAverager):
+        averager.close()
     tr.close()
 
 

@@ -109,6 +109,17 @@ class Word2Vec {
   // matrix cores (w2v_dev_set_update, W2V_UPDATE_SHARED_NEGATIVES) instead of
   // the reference's per-pair update; sg + ns only, negative <= 15, window <= 8
   bool shared_negatives = false;
+  // Data-parallel replicas (BASELINE configs[3]): with >= 2 entries, train()
+  // runs one full model replica per listed HIP device (a device may repeat:
+  // replicas sharing one GPU), each on a contiguous shard of every epoch's
+  // shuffled sentence order, and averages them (include/w2v_dev.h w2v_group_*:
+  // RCCL all-reduce over xGMI) every sync_words in-vocab words of the largest
+  // shard (0 = once per epoch), overlapped with the next round's training
+  // unless overlap_average is false. Empty = one device (gpu_device).
+  std::vector<int> gpu_devices;
+  int64_t sync_words = 0;
+  bool overlap_average = true;
+  int replica_mode = W2V_GROUP_SUM;  // w2v_group_set_mode: how the replicas' updates combine
   bool verbose = true;       // progress line per epoch (the reference prints one
                              // every 100 sentences, Word2Vec.cpp:382-386)
   // Train on a corpus that is already token ids (no strings): ids index
@@ -126,6 +137,13 @@ class Word2Vec {
   // build_sample of a corpus file as token ids (what train_file trains on).
   void file_samples(const std::string& path, const std::string& format, int threads, std::vector<int32_t>& ids,
                     std::vector<int64_t>& offsets, int64_t& train_words);
+  // Checkpoints between train() calls: W, C, synapses1, the
+  // word counter and the generator state. After load_checkpoint the next
+  // train() / train_ids() / train_file() continues from the restored weights
+  // (no init_weights) with current_words starting at the saved count.
+  void save_checkpoint(const std::string& path);
+  void load_checkpoint(const std::string& path);
+  int64_t current_words() const { return cur_words_; }
   // Last device error (empty if none).
   std::string last_error;
 
@@ -134,16 +152,21 @@ class Word2Vec {
   w2v_dev_config dev_cfg_{};        // configuration dev_ was created with
   bool dev_vocab_stale_ = true;     // vocab products changed since the last upload
   int64_t cur_words_ = 0;           // current_words after the last train call
+  bool resume_ = false;             // load_checkpoint: the next train continues (no init_weights)
+  int64_t start_words_ = 0;         //   ... from this current_words
 
   bool uses_C() const;
   void finish_vocab(std::unordered_map<std::string, int>& tally);
   void ensure_device();
   void upload_vocab_products();
+  void upload_vocab_to(w2v_dev* d);
+  void apply_policy(w2v_dev* d);
+  void run_epochs_replicas(const std::vector<int32_t>& ids, const std::vector<int64_t>& offsets, int64_t train_words);
   void check(int rc, const char* what);
   void run_epochs(const std::vector<int32_t>& ids, const std::vector<int64_t>& offsets, int64_t train_words);
   void append_reference_draws(const std::vector<int32_t>& ids, const std::vector<int64_t>& offsets,
                               const std::vector<long>& order, std::vector<uint32_t>& stream,
-                              std::vector<int64_t>& stream_off, int64_t epoch);
+                              std::vector<int64_t>& stream_off, int64_t epoch, std::vector<int32_t>* negs = nullptr);
   void train_one_sentence(std::vector<Word*>& sentence, float alpha, bool cbow);
   void apply_rows(RMatrixXf& M, int which, const std::vector<size_t>& rows, const std::vector<uint8_t>& codes,
                   RowVectorXf& x, RowVectorXf& grad, float alpha, bool hs_form);

@@ -37,6 +37,7 @@ extern "C" {
 #define W2V_ERR_STATE 3       /* call out of order (e.g. train before upload) */
 #define W2V_ERR_UNSUPPORTED 4 /* configuration outside the kernels' range */
 #define W2V_ERR_DIVERGED 5    /* training produced non-finite values (w2v_dev_stats.nonfinite) */
+#define W2V_ERR_COMM 6        /* an RCCL call failed (w2v_group_*) */
 
 /* RNG modes for the training kernels. */
 #define W2V_RNG_PHILOX 0 /* counter-based Philox4x32-10 per (epoch, sentence, position, slot, k) */
@@ -119,6 +120,13 @@ int w2v_dev_upload_table(w2v_dev* h, const uint32_t* table, int64_t n);
  * W and C have V rows, synapses1 V-1. NULL skips a matrix. */
 int w2v_dev_upload_model(w2v_dev* h, const float* W, const float* C, const float* syn1);
 int w2v_dev_download_model(w2v_dev* h, float* W, float* C, float* syn1);
+/* Row-sparse transfers: rows[k] of matrix `which` (0 = W, 1 = C, 2 =
+ * synapses1) <-> data[k * word_dim .. +word_dim) (host, dense). The per-call
+ * methods (Word2Vec::train_sentence_*, Word2Vec.h:83-84) move only the rows a
+ * sentence's update can touch instead of the whole model. The first call
+ * allocates the resident model (its other rows are not initialised). */
+int w2v_dev_upload_rows(w2v_dev* h, int32_t which, const int32_t* rows, int64_t n, const float* data);
+int w2v_dev_download_rows(w2v_dev* h, int32_t which, const int32_t* rows, int64_t n, float* data);
 /* Train on caller-owned device matrices instead (e.g. torch tensors that an
  * RCCL all-reduce also touches): rows of `pitch` floats (pitch % 4 == 0,
  * pitch >= word_dim, 16-B aligned bases), padding columns zero. NULL for a
@@ -142,6 +150,13 @@ int w2v_dev_upload_replay(w2v_dev* h, const uint32_t* stream, int64_t n,
 /* The reference's shared current_words counter (Word2Vec.cpp:359,393). */
 int w2v_dev_set_progress(w2v_dev* h, int64_t current_words);
 int w2v_dev_get_progress(w2v_dev* h, int64_t* current_words);
+/* The same, enqueued on the handle's stream (ordered between training slices). */
+int w2v_dev_set_progress_async(w2v_dev* h, int64_t current_words);
+/* Replace train_words (Word2Vec.cpp:362-363), the denominator of the alpha
+ * schedule (:379-380). A replica that trains 1/N of the corpus with its
+ * counter at (global words) / N follows the global schedule with
+ * train_words = (global raw tokens) / N. */
+int w2v_dev_set_train_words(w2v_dev* h, int64_t train_words);
 
 /* Replaces: one iteration of train()'s epoch loop (Word2Vec.cpp:371-395):
  * the sentences are visited in `order` (host array of n_sentences sentence
@@ -158,6 +173,13 @@ int w2v_dev_train_epoch_async(w2v_dev* h, int32_t epoch, const int64_t* order_de
  * arbitrary slice of an epoch's order), enqueued on the handle's stream: lets a
  * caller cut an epoch into rounds between model-averaging points. */
 int w2v_dev_train_sentences_async(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int64_t count);
+/* An epoch's sentence order (host array, n <= n_sentences ids) kept on the
+ * device, and a slice [first, first + count) of it trained, enqueued on the
+ * handle's stream: how a host loop cuts an epoch into rounds between
+ * averaging points without device pointers. set_order waits for the work
+ * already enqueued (it may still read the previous order). */
+int w2v_dev_set_order(w2v_dev* h, const int64_t* order, int64_t n);
+int w2v_dev_train_slice_async(w2v_dev* h, int32_t epoch, int64_t first, int64_t count);
 int w2v_dev_synchronize(w2v_dev* h);
 int w2v_dev_read_stats(w2v_dev* h, w2v_dev_stats* stats); /* cumulative; synchronizes */
 int w2v_dev_reset_stats(w2v_dev* h);
@@ -197,6 +219,10 @@ int w2v_dev_set_hot_auto(w2v_dev* h, float tau_rows, float tau_nodes);
  * Huffman nodes, LDS-private output rows, LDS-private context rows. */
 int w2v_dev_policy(w2v_dev* h, int64_t* hot_rows, int64_t* hot_nodes, int32_t* private_rows, int32_t* context_rows);
 int w2v_dev_set_private_rows(w2v_dev* h, int32_t n);
+/* With private_rows = -1: privatise only the rows (Huffman nodes for HS, and
+ * CBOW context rows) a center updates at least `mu` times on average, from
+ * the corpus statistics (0 = no rate limit: as many as fit, <= 64). */
+int w2v_dev_set_private_rate(w2v_dev* h, float mu);
 /* flush_centers: workgroup centers between flushes (0 = auto: 1024 for NS, 64
  * for HS); average_over: the concurrency a private row's summed deltas are
  * scaled down to (default 8; 0 = plain sum). */
@@ -245,6 +271,48 @@ int w2v_dev_set_fixed_alpha(w2v_dev* h, float alpha);
  * double, :241-242) or the NS one (g = (label - f) * alpha, :263-264). */
 int w2v_dev_apply_rows(w2v_dev* h, float* rows, const uint8_t* codes, int32_t n, const float* x,
                        float* grad, float alpha, int32_t hs_form);
+
+/* ---------------------------------------------------------------------------
+ * Multi-GPU data parallelism (BASELINE configs[3], configs[4] at 2/4/8 GPUs;
+ * new: the reference has only OpenMP threads on one model, Word2Vec.cpp:375-394).
+ * Every replica (a w2v_dev handle with its model resident; all replicas start
+ * from the same weights) trains its shard of the sentences;
+ * w2v_group_average_async exchanges what the replicas learned since the last
+ * exchange, ordered on each replica's stream after the work enqueued so far:
+ * D_i = M_i - P, A = sum_i D_i (one ncclAllReduce per matrix over xGMI),
+ * M_i = P + A / c per row: W2V_GROUP_SUM (default) c = 1 (every update
+ * counts once, as in the reference's one shared model);
+ * W2V_GROUP_ROW_AVERAGE c = the number of replicas that changed the row;
+ * W2V_GROUP_AVERAGE c = R (model averaging: the mean of the replicas). One
+ * process may drive several replicas (one per device: ncclCommInitAll), or
+ * each process one or more with ranks from a shared unique id (one process
+ * per GPU: rank 0 calls w2v_group_unique_id and hands the bytes to the others
+ * out of band). Replicas on ONE device in one process are averaged by a
+ * kernel instead (RCCL cannot put two ranks on one GPU).
+ * Overlap (w2v_group_set_overlap(g, 1)): the all-reduce runs on a
+ * communication stream while the next slice trains, and is folded in at the
+ * next call (M += A / c - D: the other replicas' updates): the exchange is
+ * delayed by one round, hidden behind compute. w2v_group_finish folds in the
+ * last pending exchange and synchronises. The caller keeps the alpha schedule
+ * global (w2v_dev_set_progress_async, w2v_dev_set_train_words).
+ * ------------------------------------------------------------------------- */
+#define W2V_GROUP_ID_BYTES 128
+typedef struct w2v_group w2v_group;
+int w2v_group_unique_id(uint8_t* id /* W2V_GROUP_ID_BYTES */);
+/* members: the n handles this process drives (same model shape). unique_id
+ * NULL: all replicas are in this process (nranks = n). Otherwise this
+ * process's replicas are ranks [first_rank, first_rank + n) of nranks. */
+int w2v_group_create(w2v_dev** members, int32_t n, const uint8_t* unique_id, int32_t nranks, int32_t first_rank,
+                     w2v_group** out);
+void w2v_group_destroy(w2v_group* g);
+int w2v_group_set_overlap(w2v_group* g, int32_t on);
+#define W2V_GROUP_SUM 0
+#define W2V_GROUP_AVERAGE 1
+#define W2V_GROUP_ROW_AVERAGE 2
+int w2v_group_set_mode(w2v_group* g, int32_t mode);
+int w2v_group_average_async(w2v_group* g);
+int w2v_group_finish(w2v_group* g);
+int w2v_group_info(w2v_group* g, int32_t* nranks, int32_t* local, int32_t* overlap, int64_t* rounds);
 
 #ifdef __cplusplus
 }

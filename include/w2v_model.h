@@ -32,6 +32,9 @@ void w2v_model_update_policy(w2v_model* m, int64_t hot_rows, int32_t private_row
 void w2v_model_context_policy(w2v_model* m, int32_t context_rows, int32_t context_flush);
 /* Word2Vec::shared_negatives (configs[4] minibatch skip-gram; include/w2v_dev.h w2v_dev_set_update). */
 void w2v_model_set_shared_negatives(w2v_model* m, int32_t on);
+/* Word2Vec::gpu_devices / sync_words / overlap_average: n >= 2 devices train
+ * data-parallel replicas (a device may repeat); n < 2 = one device. */
+void w2v_model_replicas(w2v_model* m, const int32_t* devices, int32_t n, int64_t sync_words, int32_t overlap);
 
 /* Sentences as text: one per line, whitespace-separated tokens (line_docs format). */
 int w2v_model_build_vocab(w2v_model* m, const char* text, int64_t len);
@@ -75,6 +78,11 @@ int w2v_model_hierarchical_softmax(w2v_model* m, int64_t word, float* x, float* 
 int w2v_model_save(w2v_model* m, const char* path, int32_t which, int32_t binary);
 int w2v_model_load(w2v_model* m, const char* path, int32_t binary);
 int w2v_model_save_vocab(w2v_model* m, const char* path);
+/* Word2Vec::save_checkpoint / load_checkpoint (W, C, synapses1, current_words,
+ * generator state; the next train continues from them) and current_words(). */
+int w2v_model_save_checkpoint(w2v_model* m, const char* path);
+int w2v_model_load_checkpoint(w2v_model* m, const char* path);
+int64_t w2v_model_current_words(w2v_model* m);
 int w2v_model_read_vocab(w2v_model* m, const char* path);
 
 #ifdef __cplusplus

@@ -4,7 +4,7 @@ from the seeded initial weights over the seeded sentence orders; the scores go
 to tests/golden/quality_paired_oracle.json. The GPU tests
 (tests/test_gpu_quality.py) train from the same start on the same draws.
 About 1 min per text8-like run; runs in parallel processes. From the repo root:
-python tests/golden/gen_quality_paired_golden.py"""
+python tests/golden/gen_quality_paired_golden.py [workers] [corpus ...]"""
 import json
 import sys
 from concurrent.futures import ProcessPoolExecutor
@@ -33,8 +33,17 @@ def one(job):
 def main(workers=4):
     from tests import paired
 
-    jobs = [(n, m, s) for n, modes in paired.PAIRED_MODES.items() for m in modes for s in paired.PAIRED_SEEDS]
-    out = {"seeds": list(paired.PAIRED_SEEDS), "planted": {}, "text8_like": {}}
+    import json as _json
+
+    only = set(sys.argv[2:])  # corpus names to (re)generate; the rest is kept
+    f = ROOT / "tests" / "golden" / "quality_paired_oracle.json"
+    out = _json.loads(f.read_text()) if f.exists() and only else {}
+    out["seeds"] = {k: list(v) for k, v in paired.PAIRED_SEEDS.items()}
+    jobs = [(n, m, s) for n, modes in paired.PAIRED_MODES.items() if not only or n in only for m in modes
+            for s in paired.PAIRED_SEEDS[n]]
+    for n in paired.PAIRED_MODES:
+        if not only or n in only:
+            out[n] = {}
     with ProcessPoolExecutor(workers) as ex:
         for name, mode, r in ex.map(one, jobs):
             out[name].setdefault(mode, []).append(r)

@@ -17,12 +17,22 @@ from tests.golden.gen_quality_zipf_golden import ZCORPUS, ZTRAIN, zalpha
 from tests.harness import device_config, oracle_run
 from tests.quality import planted_corpus, planted_zipf_corpus
 
-PAIRED_SEEDS = (1, 2, 3)
-PAIRED_MODES = {"planted": ("sg_ns", "sg_hs", "cbow_ns", "cbow_hs"), "text8_like": ("sg_ns", "cbow_hs")}
+# corpus -> seeds; text8_small is a text8-like corpus of 2 M tokens (20 K filler
+# types, 30 % planted positions, so one epoch learns the relations), for the
+# one-wavefront runs (one wave trains ~60 K words/s: 10 M tokens take minutes)
+PAIRED_SEEDS = {"planted": (1, 2, 3), "text8_like": (1, 2, 3), "text8_small": (1,)}
+PAIRED_MODES = {"planted": ("sg_ns", "sg_hs", "cbow_ns", "cbow_hs"), "text8_like": ("sg_ns", "cbow_hs"),
+                "text8_small": ("sg_ns", "cbow_hs")}
+ONE_WAVE_CORPORA = ("planted", "text8_small")
+FULL_CORPORA = ("planted", "text8_like")
 
 
 def corpus(name):
-    return planted_corpus(**CORPUS) if name == "planted" else planted_zipf_corpus(**ZCORPUS)
+    if name == "planted":
+        return planted_corpus(**CORPUS)
+    if name == "text8_small":
+        return planted_zipf_corpus(n_tokens=2_000_000, sent_len=1000, filler=20_000, planted_frac=0.3, seed=0)
+    return planted_zipf_corpus(**ZCORPUS)
 
 
 def params(name, mode):
@@ -89,6 +99,8 @@ def train_gpu_paired(name, mode, seed, sents, max_waves=0, stats=None, policy=No
         d.set_hot_auto(pol.get("hot_tau_rows", 1.0), pol.get("hot_tau_nodes", 1.0))
     if "private_rows" in pol:
         d.set_private_rows(pol["private_rows"])
+    if "private_rate" in pol:
+        d.set_private_rate(pol["private_rate"])
     if "flush_centers" in pol or "private_average" in pol:
         d.set_private_sync(pol.get("flush_centers", 0), pol.get("private_average", 8.0))
     if "context_rows" in pol or "context_flush" in pol:

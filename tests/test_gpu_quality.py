@@ -7,7 +7,9 @@ weights on the oracle's own Philox draws and sentence orders, so the corpus's
 seed-to-seed variance cancels and what is measured is the schedule:
   * one wavefront through the parallel kernel (the same code path as full
     concurrency, LDS-privatised rows and all): two-sided, |delta| <= 1 point
-    (north_star's "within +-1 point"), per corpus and mode, mean of 3 seeds;
+    (north_star's "within +-1 point"), per corpus and mode (planted: mean of
+    3 seeds; the text8-like corpus at 2 M tokens: one seed, since one wave
+    trains ~60 K words/s);
   * full concurrency with the default update policy: one-sided, the mean
     delta must not fall below -1 (its damped, aggregated updates of the
     frequent rows score above the sequential reference on these corpora,
@@ -88,13 +90,13 @@ def _paired_delta(name, mode, max_waves):
     return d, got, ref
 
 
-@pytest.mark.parametrize("name,mode", [(n, m) for n, ms in paired.PAIRED_MODES.items() for m in ms])
+@pytest.mark.parametrize("name,mode", [(n, m) for n in paired.ONE_WAVE_CORPORA for m in paired.PAIRED_MODES[n]])
 def test_quality_paired_one_wave_within_1(name, mode):
     d, got, ref = _paired_delta(name, mode, max_waves=1)
     assert abs(d[0]) <= 1.0 and abs(d[1]) <= 1.0, (name, mode, got, ref)
 
 
-@pytest.mark.parametrize("name,mode", [(n, m) for n, ms in paired.PAIRED_MODES.items() for m in ms])
+@pytest.mark.parametrize("name,mode", [(n, m) for n in paired.FULL_CORPORA for m in paired.PAIRED_MODES[n]])
 def test_quality_paired_full_concurrency_not_below(name, mode):
     d, got, ref = _paired_delta(name, mode, max_waves=0)
     assert d[0] >= -1.0 and d[1] >= -1.0, (name, mode, got, ref)

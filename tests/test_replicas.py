@@ -1,7 +1,8 @@
 """Multi-rank logic of word2vec_amd/replicas.py on CPU with gloo (world 2 and 3):
-shards partition the corpus, averaging is the exact mean, the global progress
-is the sum of the ranks' counters, and the round loop drives a trainer the
-way the GPU path does (a fake trainer stands in for the HIP handle)."""
+shards partition the corpus, averaging is the exact mean, the per-round global
+word counts are the sum over ranks, and the round loop drives a trainer the
+way the GPU path does (a fake trainer stands in for the HIP handle, the
+torch/gloo averager for the native RCCL group)."""
 import os
 import socket
 
@@ -10,7 +11,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from word2vec_amd.replicas import ReplicaGroup, n_rounds, round_slices, shard_range, train_rounds
+from word2vec_amd.replicas import (TorchAverager, global_round_words, local_round_words, n_rounds, round_slices,
+                                   shard_range, train_rounds)
 
 
 def test_shard_range_partitions():
@@ -45,19 +47,25 @@ def _free_port():
     return p
 
 
+def test_local_round_words():
+    off = [0, 3, 5, 9, 10]  # sentence lengths 3, 2, 4, 1
+    assert local_round_words(off, [2, 0, 3, 1], 2) == [7, 3]
+    assert local_round_words(off, [0, 1, 2, 3], 3) == [3, 2, 5]
+    assert sum(local_round_words(off, [3, 2, 1, 0], 1)) == 10
+
+
 class FakeTrainer:
     """Adds (rank+1) to every replica element per trained sentence and counts
-    10 words per sentence, like a device handle bound to the tensors."""
+    10 words per sentence, like a device handle bound to the tensors; records
+    the progress values the round loop sets."""
 
     def __init__(self, tensors, rank):
         self.t, self.rank, self.words = tensors, rank, 0
-        self.seen = []
+        self.seen, self.progress = [], []
 
-    def set_progress(self, w):
+    def set_progress_async(self, w):
         self.words = w
-
-    def get_progress(self):
-        return self.words
+        self.progress.append(w)
 
     def train_sentences_async(self, epoch, ptr, count):
         self.seen.append(count)
@@ -72,20 +80,21 @@ def _worker(rank, world, port, out):
     try:
         W = torch.full((4, 8), float(rank), dtype=torch.float32)
         C = torch.arange(32, dtype=torch.float32).reshape(4, 8) * (rank + 1)
-        g = ReplicaGroup([W, C], world)
+        g = TorchAverager([W, C], world)
         g.average()
         mean_rank = sum(range(world)) / world
         assert torch.allclose(W, torch.full_like(W, mean_rank))
         assert torch.allclose(C, torch.arange(32, dtype=torch.float32).reshape(4, 8) * (world + 1) / 2)
-        assert g.global_progress(rank + 1, "cpu") == world * (world + 1) // 2
-        # round loop: uneven shards of 15 sentences, sync every 3 of the largest
+        # round loop: uneven shards of 15 sentences of 10 words, sync every 3 of the largest
         lo, hi = shard_range(15, rank, world)
         order = torch.arange(lo, hi, dtype=torch.int64)
+        R = n_rounds(15, world, 3)
+        off = [10 * k for k in range(16)]
+        rw = global_round_words(local_round_words(off, order.tolist(), R), world)
         W.zero_()
         tr = FakeTrainer([W], rank)
-        total = train_rounds(tr, ReplicaGroup([W], world), order, 0, n_rounds(15, world, 3), "cpu",
-                             progress_base=100)
-        out.put((rank, tr.seen, total, W[0, 0].item()))
+        total = train_rounds(tr, TorchAverager([W], world), order, 0, R, 100, rw, world)
+        out.put((rank, tr.seen, total, W[0, 0].item(), tr.progress, rw))
     finally:
         dist.destroy_process_group()
 
@@ -105,6 +114,11 @@ def test_gloo_replica_averaging_and_rounds(world):
     # every rank ran the same number of rounds; progress = 100 + 10 words x 15 sentences
     totals = {r[2] for r in res}
     assert totals == {100 + 10 * 15}
+    # the counter each rank starts a round from is the global count / world
+    rw = res[0][5]
+    assert sum(rw) == 150 and all(r[5] == rw for r in res)
+    starts = [100 + sum(rw[:k]) for k in range(len(rw))]
+    assert all(r[4] == [s // world for s in starts] for r in res)
     # the replica after the rounds is identical on every rank and equals the
     # sequence of averaged round updates
     vals = {round(r[3], 4) for r in res}

@@ -23,7 +23,7 @@ def parse_policy(p):
     out = {}
     for kv in p.split(","):
         k, v = kv.split("=")
-        out[k] = float(v) if k in ("private_average", "hot_tau_rows", "hot_tau_nodes") else int(v)
+        out[k] = float(v) if k in ("private_average", "hot_tau_rows", "hot_tau_nodes", "private_rate") else int(v)
     return out
 
 

@@ -20,6 +20,11 @@ W2V_ERR_HIP = 2
 W2V_ERR_STATE = 3
 W2V_ERR_UNSUPPORTED = 4
 W2V_ERR_DIVERGED = 5
+W2V_ERR_COMM = 6
+W2V_GROUP_ID_BYTES = 128
+W2V_GROUP_SUM = 0
+W2V_GROUP_AVERAGE = 1
+W2V_GROUP_ROW_AVERAGE = 2
 W2V_RNG_PHILOX = 0
 W2V_RNG_REPLAY = 1
 W2V_SCHED_PARALLEL = 0
@@ -81,16 +86,22 @@ SIGNATURES = {
     "w2v_dev_upload_table": (C.c_int, [_P, _P, _I64]),
     "w2v_dev_upload_model": (C.c_int, [_P, _P, _P, _P]),
     "w2v_dev_download_model": (C.c_int, [_P, _P, _P, _P]),
+    "w2v_dev_upload_rows": (C.c_int, [_P, _I32, _P, _I64, _P]),
+    "w2v_dev_download_rows": (C.c_int, [_P, _I32, _P, _I64, _P]),
     "w2v_dev_bind_model": (C.c_int, [_P, _P, _P, _P, _I64]),
     "w2v_dev_model_layout": (C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), C.POINTER(_I64)]),
     "w2v_dev_upload_corpus": (C.c_int, [_P, _P, _I64, _P, _I64, _I64]),
     "w2v_dev_upload_replay": (C.c_int, [_P, _P, _I64, _P, _I64]),
     "w2v_dev_set_progress": (C.c_int, [_P, _I64]),
     "w2v_dev_get_progress": (C.c_int, [_P, C.POINTER(_I64)]),
+    "w2v_dev_set_progress_async": (C.c_int, [_P, _I64]),
+    "w2v_dev_set_train_words": (C.c_int, [_P, _I64]),
     "w2v_dev_train_epoch": (C.c_int, [_P, _I32, _P, C.POINTER(DevStats)]),
     "w2v_dev_train_epoch_async": (C.c_int, [_P, _I32, _P]),
     "w2v_dev_train_sentences_async": (C.c_int, [_P, _I32, _P, _I64]),
     "w2v_dev_synchronize": (C.c_int, [_P]),
+    "w2v_dev_set_order": (C.c_int, [_P, _P, _I64]),
+    "w2v_dev_train_slice_async": (C.c_int, [_P, _I32, _I64, _I64]),
     "w2v_dev_read_stats": (C.c_int, [_P, C.POINTER(DevStats)]),
     "w2v_dev_reset_stats": (C.c_int, [_P]),
     "w2v_dev_set_fixed_alpha": (C.c_int, [_P, _F]),
@@ -98,11 +109,20 @@ SIGNATURES = {
     "w2v_dev_set_hot_auto": (C.c_int, [_P, _F, _F]),
     "w2v_dev_policy": (C.c_int, [_P, C.POINTER(_I64), C.POINTER(_I64), C.POINTER(_I32), C.POINTER(_I32)]),
     "w2v_dev_set_private_rows": (C.c_int, [_P, _I32]),
+    "w2v_dev_set_private_rate": (C.c_int, [_P, _F]),
     "w2v_dev_set_private_sync": (C.c_int, [_P, _I32, _F]),
     "w2v_dev_set_context_private": (C.c_int, [_P, _I32, _I32]),
     "w2v_dev_set_max_waves": (C.c_int, [_P, _I64]),
     "w2v_dev_set_update": (C.c_int, [_P, _I32]),
     "w2v_dev_apply_rows": (C.c_int, [_P, _P, _P, _I32, _P, _P, _F, _I32]),
+    "w2v_group_unique_id": (C.c_int, [_P]),
+    "w2v_group_create": (C.c_int, [_P, _I32, _P, _I32, _I32, C.POINTER(_P)]),
+    "w2v_group_destroy": (None, [_P]),
+    "w2v_group_set_overlap": (C.c_int, [_P, _I32]),
+    "w2v_group_set_mode": (C.c_int, [_P, _I32]),
+    "w2v_group_average_async": (C.c_int, [_P]),
+    "w2v_group_finish": (C.c_int, [_P]),
+    "w2v_group_info": (C.c_int, [_P, C.POINTER(_I32), C.POINTER(_I32), C.POINTER(_I32), C.POINTER(_I64)]),
 }
 
 _lib = None

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "w2v_dev.h"
+#include "w2v_dev_internal.hpp"
 #include "w2v_kernels.hpp"
 #include "w2v_launch.hpp"
 #include "w2v_shared.hpp"
@@ -77,6 +78,7 @@ struct Knobs {
   int sn_occ = 0;                // W2V_SN_OCC: shared-negatives kernel's waves per SIMD
   int64_t sn_coherent_rows = -1; // W2V_SN_COHERENT_ROWS
   int64_t sn_atomic_rows = -1;   // W2V_SN_ATOMIC_ROWS
+  int scale_resident = 0;        // W2V_SCALE_RESIDENT=1: flush scales from the chip's resident workgroups, not the launch's grid
   std::string desc;              // "NAME=value ..." of the variables that were set
 };
 
@@ -94,6 +96,7 @@ static Knobs read_knobs() {
   if (const char* v = get("W2V_SN_OCC")) k.sn_occ = std::max(0, std::atoi(v));
   if (const char* v = get("W2V_SN_COHERENT_ROWS")) k.sn_coherent_rows = std::max<int64_t>(0, std::atoll(v));
   if (const char* v = get("W2V_SN_ATOMIC_ROWS")) k.sn_atomic_rows = std::max<int64_t>(0, std::atoll(v));
+  if (const char* v = get("W2V_SCALE_RESIDENT")) k.scale_resident = std::atoi(v) != 0;
   return k;
 }
 
@@ -129,6 +132,7 @@ struct w2v_dev {
   int64_t n_tok = 0, n_sent = 0, train_words = 0;
   int64_t max_len = 0;        // longest sentence (tokens)
   int64_t* order = nullptr;
+  int64_t n_order = 0;        // entries of `order` set by w2v_dev_set_order
   uint32_t* replay = nullptr;
   int64_t* replay_off = nullptr;
   int64_t n_replay_off = 0;
@@ -137,6 +141,8 @@ struct w2v_dev {
   float* scratch_f = nullptr;      // x | grad | rows for apply_rows
   uint8_t* scratch_codes = nullptr;
   int64_t scratch_n = 0;           // floats in scratch_f
+  float* xfer_f = nullptr;         // row-sparse transfers: packed rows | row ids
+  int64_t xfer_n = 0;
   float fixed_alpha = 0.0f;
   int32_t rng = W2V_RNG_PHILOX;
   uint64_t seed = 0;
@@ -160,10 +166,16 @@ struct w2v_dev {
   std::vector<double> f, fk, node_f, node_fk;
   double hot_tau_rows = 1.0;        // automatic hot rows: expected concurrent updates threshold, W / C rows
   double hot_tau_nodes = 1.0;       //   ... and Huffman nodes
+  double private_rate = 0.0;        // > 0: privatise only rows updated >= this many times per center (private_by_rate)
   // the policy the last parallel launch used (w2v_dev_policy)
   int64_t last_hot_rows = 0, last_hot_nodes = 0;
   int32_t last_priv = 0, last_ctx = 0;
 };
+
+namespace w2v {
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+DevInfo dev_info(const w2v_dev* h) { return DevInfo{h->device, h->stream, h->V}; }
+}  // namespace w2v
 
 // Per-word and per-node shares of the corpus (cached until the next upload).
 static void row_stats(w2v_dev* h) {
@@ -319,7 +331,7 @@ void w2v_dev_destroy(w2v_dev* h) {
   dfree(h->keep); dfree(h->table); dfree(h->codes); dfree(h->points); dfree(h->coff);
   dfree(h->ids); dfree(h->soff); dfree(h->order); dfree(h->replay); dfree(h->replay_off);
   dfree(h->counters); dfree(h->work);
-  dfree(h->scratch_f); dfree(h->scratch_codes);
+  dfree(h->scratch_f); dfree(h->scratch_codes); dfree(h->xfer_f);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -356,6 +368,7 @@ int w2v_dev_set_schedule(w2v_dev* h, int32_t s) {
 
 int w2v_dev_upload_vocab(w2v_dev* h, int64_t V, const float* keep, const int64_t* bounds,
                          const uint8_t* codes, const int32_t* points, const int64_t* coff) {
+  w2v::Range range_("w2v_dev_upload_vocab");
   if (!h || !keep) return fail(W2V_ERR_ARG, "w2v_dev_upload_vocab: null argument");
   if (V < 1 || V > (int64_t)INT32_MAX) return fail(W2V_ERR_ARG, "vocab_size out of range");
   if (h->cfg.hs && V < 2) return fail(W2V_ERR_ARG, "hs needs vocab_size >= 2");
@@ -486,6 +499,7 @@ static int ensure_model(w2v_dev* h) {
 }
 
 int w2v_dev_upload_model(w2v_dev* h, const float* W, const float* C, const float* S) {
+  w2v::Range range_("w2v_dev_upload_model");
   if (!h) return fail(W2V_ERR_ARG, "null handle");
   if (set_device(h)) return W2V_ERR_HIP;
   int rc = ensure_model(h);
@@ -506,6 +520,7 @@ int w2v_dev_upload_model(w2v_dev* h, const float* W, const float* C, const float
 }
 
 int w2v_dev_download_model(w2v_dev* h, float* W, float* C, float* S) {
+  w2v::Range range_("w2v_dev_download_model");
   if (!h) return fail(W2V_ERR_ARG, "null handle");
   if (!h->W) return fail(W2V_ERR_STATE, "no model on the device");
   if (set_device(h)) return W2V_ERR_HIP;
@@ -516,6 +531,72 @@ int w2v_dev_download_model(w2v_dev* h, float* W, float* C, float* S) {
   if (S && h->S && h->V > 1)
     HIP_TRY(hipMemcpy2D(S, d * sizeof(float), h->S, dp, d * sizeof(float), h->V - 1, hipMemcpyDeviceToHost));
   return W2V_OK;
+}
+
+namespace w2v {
+// rows[k] of M (pitch-padded) <-> packed[k] (dim floats), one wave per row.
+__global__ void scatter_rows_kernel(float* M, int64_t pitch, int d, const int32_t* rows, int64_t n, const float* packed) {
+  const int64_t k = blockIdx.x;
+  if (k >= n) return;
+  float* dst = M + (int64_t)rows[k] * pitch;
+  const float* src = packed + k * d;
+  for (int e = threadIdx.x; e < d; e += blockDim.x) dst[e] = src[e];
+}
+__global__ void gather_rows_kernel(const float* M, int64_t pitch, int d, const int32_t* rows, int64_t n, float* packed) {
+  const int64_t k = blockIdx.x;
+  if (k >= n) return;
+  const float* src = M + (int64_t)rows[k] * pitch;
+  float* dst = packed + k * d;
+  for (int e = threadIdx.x; e < d; e += blockDim.x) dst[e] = src[e];
+}
+}  // namespace w2v
+
+// Row-sparse transfer between host rows and one resident matrix: the per-call
+// methods (train_sentence_*) move only the rows a sentence's update can touch.
+static int transfer_rows(w2v_dev* h, int32_t which, const int32_t* rows, int64_t n, float* data, bool up) {
+  if (!h || (n > 0 && (!rows || !data))) return fail(W2V_ERR_ARG, "row transfer: null argument");
+  if (n < 0 || n > (int64_t)INT32_MAX) return fail(W2V_ERR_ARG, "row transfer: bad row count");
+  if (which < 0 || which > 2) return fail(W2V_ERR_ARG, "row transfer: which must be 0 (W), 1 (C) or 2 (synapses1)");
+  if (set_device(h)) return W2V_ERR_HIP;
+  if (int rc = ensure_model(h)) return rc;
+  float* M = which == 0 ? h->W : which == 1 ? h->C : h->S;
+  const int64_t nrows = which == 2 ? h->V - 1 : h->V;
+  if (!M) return fail(W2V_ERR_ARG, "row transfer: this configuration has no such matrix");
+  for (int64_t k = 0; k < n; ++k)
+    if (rows[k] < 0 || rows[k] >= nrows) return fail(W2V_ERR_ARG, "row transfer: row index out of range");
+  if (n == 0) return W2V_OK;
+  const int d = h->cfg.word_dim;
+  const int64_t need = n * d + n + 1;  // packed rows, then the row ids (int32 in float slots)
+  if (h->xfer_n < need) {
+    dfree(h->xfer_f);
+    HIP_TRY(hipMalloc(&h->xfer_f, need * sizeof(float)));
+    h->xfer_n = need;
+  }
+  float* packed = h->xfer_f;
+  int32_t* drows = reinterpret_cast<int32_t*>(h->xfer_f + n * d);
+  HIP_TRY(hipMemcpyAsync(drows, rows, n * sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
+  if (up) {
+    HIP_TRY(hipMemcpyAsync(packed, data, (size_t)n * d * sizeof(float), hipMemcpyHostToDevice, h->stream));
+    hipLaunchKernelGGL(w2v::scatter_rows_kernel, dim3((unsigned)n), dim3(256), 0, h->stream, M, h->pitch, d, drows, n,
+                       packed);
+    HIP_TRY(hipGetLastError());
+  } else {
+    hipLaunchKernelGGL(w2v::gather_rows_kernel, dim3((unsigned)n), dim3(256), 0, h->stream, M, h->pitch, d, drows, n,
+                       packed);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(data, packed, (size_t)n * d * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  h->model_ready = true;
+  return W2V_OK;
+}
+
+int w2v_dev_upload_rows(w2v_dev* h, int32_t which, const int32_t* rows, int64_t n, const float* data) {
+  return transfer_rows(h, which, rows, n, const_cast<float*>(data), true);
+}
+
+int w2v_dev_download_rows(w2v_dev* h, int32_t which, const int32_t* rows, int64_t n, float* data) {
+  return transfer_rows(h, which, rows, n, data, false);
 }
 
 int w2v_dev_bind_model(w2v_dev* h, float* dW, float* dC, float* dS, int64_t pitch) {
@@ -550,6 +631,7 @@ int w2v_dev_model_layout(w2v_dev* h, float** dW, float** dC, float** dS, int64_t
 
 int w2v_dev_upload_corpus(w2v_dev* h, const int32_t* ids, int64_t n_tok, const int64_t* soff,
                           int64_t n_sent, int64_t train_words) {
+  w2v::Range range_("w2v_dev_upload_corpus");
   if (!h || !soff || (n_tok > 0 && !ids)) return fail(W2V_ERR_ARG, "w2v_dev_upload_corpus: null argument");
   if (n_sent < 0 || n_tok < 0 || n_sent > (int64_t)UINT32_MAX - 1)
     return fail(W2V_ERR_ARG, "corpus sizes out of range");
@@ -576,6 +658,7 @@ int w2v_dev_upload_corpus(w2v_dev* h, const int32_t* ids, int64_t n_tok, const i
   HIP_TRY(hipMalloc(&h->order, (n_sent > 0 ? n_sent : 1) * sizeof(int64_t)));
   h->n_tok = n_tok;
   h->n_sent = n_sent;
+  h->n_order = 0;
   h->max_len = max_len;
   h->train_words = train_words;
   h->tok_count.swap(hist);
@@ -605,6 +688,27 @@ int w2v_dev_set_progress(w2v_dev* h, int64_t cw) {
   unsigned long long v = (unsigned long long)cw;
   HIP_TRY(hipMemcpyAsync(h->counters, &v, sizeof(v), hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
+  return W2V_OK;
+}
+
+namespace w2v {
+__global__ void set_counter_kernel(unsigned long long* p, unsigned long long v) { *p = v; }
+}  // namespace w2v
+
+int w2v_dev_set_progress_async(w2v_dev* h, int64_t cw) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (cw < 0) return fail(W2V_ERR_ARG, "current_words must be >= 0");
+  if (set_device(h)) return W2V_ERR_HIP;
+  hipLaunchKernelGGL(w2v::set_counter_kernel, dim3(1), dim3(1), 0, h->stream, h->counters, (unsigned long long)cw);
+  HIP_TRY(hipGetLastError());
+  return W2V_OK;
+}
+
+int w2v_dev_set_train_words(w2v_dev* h, int64_t train_words) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (train_words <= 0) return fail(W2V_ERR_ARG, "train_words must be > 0");
+  if (!h->corpus_ready) return fail(W2V_ERR_STATE, "upload the corpus first");
+  h->train_words = train_words;
   return W2V_OK;
 }
 
@@ -672,6 +776,44 @@ static void priv_scales(w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool shared) {
   for (int p = 0; p < a.ctx_n; ++p) a.ctx_sc[p] = sc(win1 * f(p), a.ctx_flush_every);
 }
 
+// Privatised rows by update rate (private_rate mu > 0, private_rows = -1): only
+// the output rows (Huffman nodes for HS) and CBOW context rows a center
+// updates at least mu times on average go to LDS. The LDS rows' averaged
+// flush damps every row it holds by up to 8 / workgroups whatever its rate,
+// which a row of moderate rate does not need (atomics keep its updates) and
+// which under-trains it: on a 2 M-token text8-like corpus whose planted role
+// words rank inside the top 64, 64 private rows give SG-NS analogy / similarity
+// 62.7 / 41.2 against the oracle's 69.5 / 65.4; 8 private rows 94.0 / 72.7
+// (profiles/r02q_*). Returns {output rows, context rows}.
+static std::pair<int64_t, int64_t> private_by_rate(w2v_dev* h, double mu) {
+  row_stats(h);
+  const int64_t V = h->V;
+  if (!h->stats_ok) return {64, w2v::kCtxMax};
+  const double win1 = (double)h->cfg.window + 1.0, neg = (double)h->cfg.negative;
+  const bool cbow = h->cfg.cbow != 0;
+  int64_t out = 0, ctx = 0;
+  if (h->cfg.hs) {
+    if ((int64_t)h->node_f.size() == V - 1)
+      for (int64_t j = V - 2; j >= 0 && out < w2v::kPrivMax; --j) {  // nodes nearest the root first
+        const double m = cbow ? h->node_fk[(size_t)j] : win1 * h->node_f[(size_t)j];
+        if (m < mu) break;
+        ++out;
+      }
+  } else {
+    for (int64_t r = 0; r < V && out < w2v::kPrivMax; ++r) {
+      const double u = r < (int64_t)h->table_frac.size() ? h->table_frac[(size_t)r] : 0.0;
+      const double m = cbow ? h->fk[(size_t)r] + neg * u : win1 * (h->f[(size_t)r] + neg * u);
+      if (m < mu) break;
+      ++out;
+    }
+  }
+  for (int64_t r = 0; r < V && ctx < w2v::kCtxMax && cbow; ++r) {
+    if (win1 * h->f[(size_t)r] < mu) break;
+    ++ctx;
+  }
+  return {out, ctx};
+}
+
 // Automatic hot rows (hot_rows == W2V_HOT_AUTO): the rows (and Huffman nodes)
 // whose expected number of updates in flight across the chip, waves x their
 // expected updates per center, is at least hot_tau. A row that several
@@ -708,7 +850,7 @@ static std::pair<int64_t, int64_t> auto_hot(w2v_dev* h, double waves, bool share
       const double m = cbow ? h->node_fk[(size_t)j] : win1 * h->node_f[(size_t)j];
       if (waves * m >= h->hot_tau_nodes) ++nodes;
     }
-  return {std::max<int64_t>(rows, std::min<int64_t>(V, 64)), nodes};
+  return {std::min<int64_t>(V, std::max<int64_t>(rows, 64)), nodes};
 }
 
 // The shared-negatives minibatch covers skip-gram NS only: a 16 x 16 MFMA tile
@@ -728,6 +870,26 @@ int w2v_dev_train_epoch_async(w2v_dev* h, int32_t epoch, const int64_t* order_de
   return launch_train(h, epoch, order_dev, h->n_sent);
 }
 
+int w2v_dev_set_order(w2v_dev* h, const int64_t* order, int64_t n) {
+  if (!h || (n > 0 && !order)) return fail(W2V_ERR_ARG, "w2v_dev_set_order: null argument");
+  if (!h->corpus_ready) return fail(W2V_ERR_STATE, "upload the corpus first");
+  if (n < 0 || n > h->n_sent) return fail(W2V_ERR_ARG, "order length must be in [0, n_sentences]");
+  for (int64_t k = 0; k < n; ++k)
+    if (order[k] < 0 || order[k] >= h->n_sent) return fail(W2V_ERR_ARG, "order entry out of range");
+  if (set_device(h)) return W2V_ERR_HIP;
+  HIP_TRY(hipStreamSynchronize(h->stream));  // a slice enqueued before may still read the old order
+  if (n > 0) HIP_TRY(hipMemcpy(h->order, order, n * sizeof(int64_t), hipMemcpyHostToDevice));
+  h->n_order = n;
+  return W2V_OK;
+}
+
+int w2v_dev_train_slice_async(w2v_dev* h, int32_t epoch, int64_t first, int64_t count) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (first < 0 || count < 0 || first + count > h->n_order)
+    return fail(W2V_ERR_ARG, "slice outside the order set with w2v_dev_set_order");
+  return launch_train(h, epoch, h->order + first, count);
+}
+
 int w2v_dev_train_sentences_async(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int64_t count) {
   if (!h) return fail(W2V_ERR_ARG, "null handle");
   if (!order_dev && count != h->n_sent) return fail(W2V_ERR_ARG, "a slice needs an order array");
@@ -736,6 +898,7 @@ int w2v_dev_train_sentences_async(w2v_dev* h, int32_t epoch, const int64_t* orde
 }
 
 static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int64_t count) {
+  w2v::Range range_("w2v launch");
   if (!h->vocab_ready || !h->corpus_ready) return fail(W2V_ERR_STATE, "upload vocab and corpus first");
   if (!h->model_ready) return fail(W2V_ERR_STATE, "upload the model first");
   if (h->cfg.negative > 0 && !h->table) return fail(W2V_ERR_STATE, "no unigram table on the device");
@@ -831,6 +994,11 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     const bool hs = h->cfg.hs != 0;
     const int64_t avail = hs ? h->V - 1 : h->V;
     if (P > avail) P = avail;
+    std::pair<int64_t, int64_t> by_rate{P, w2v::kCtxMax};
+    if (h->private_rate > 0.0) {
+      by_rate = private_by_rate(h, h->private_rate);
+      if (h->private_rows < 0) P = std::min(P, by_rate.first);
+    }
     if (P > 0) {
       a.priv_M = hs ? h->S : (h->cfg.cbow ? h->W : h->C);
       a.priv_lo = hs ? avail - P : 0;  // HS: the P internal nodes nearest the root (V-2)
@@ -843,6 +1011,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     int64_t Q = h->cfg.cbow ? std::min<int64_t>({fit - P, (int64_t)w2v::kCtxMax, h->V}) : 0;
     if (h->context_rows < 0 && !h->cfg.hs) Q = 0;
     if (h->context_rows >= 0) Q = std::min<int64_t>(Q, h->context_rows);
+    else if (h->private_rate > 0.0) Q = std::min(Q, by_rate.second);
     if (Q > 0) {
       a.ctx_M = h->C;
       a.ctx_n = (int32_t)Q;
@@ -872,7 +1041,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     // device-coherent rows (rows_rsrc in w2v_shared.hpp): all for hot_rows =
     // -1, else at least the rows two XCD L2s' capacity could keep resident
     const int64_t l2_rows = (int64_t)(8 << 20) / (h->pitch * (int64_t)sizeof(float));
-    int64_t g = 1;
+    int64_t g = 1, g_res = 1;
     if (h->sched == W2V_SCHED_PARALLEL) {
       int per_cu = 0;
       HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sn_fn, threads, 0));
@@ -882,19 +1051,20 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
       // collapses at 4): every center holds ~22 rows for its whole update, so
       // a small vocab's frequent rows are held by hundreds of workgroups at once.
       if (h->max_waves == 0) per_cu = std::min(per_cu, h->V < 16384 ? 1 : h->V < 524288 ? 2 : per_cu);
-      g = std::min<int64_t>((int64_t)per_cu * h->n_cu, count);
+      g_res = (int64_t)per_cu * h->n_cu;
+      g = std::min<int64_t>(g_res, count);
       if (h->max_waves > 0) g = std::max<int64_t>(1, std::min<int64_t>(g, h->max_waves / sn_waves));
     }
     // the hot rows (one updater per workgroup) take atomic deltas, as in the
     // per-pair kernel (parallel schedule only: the sequential one is exact
     // either way), and at least the rows two XCD L2s could keep resident are
     // device-coherent
-    const int64_t hot = hot_for((double)g, true).first;
+    const int64_t hot = hot_for((double)g_res, true).first;
     a.hot_wc = h->hot_rows == -1 ? h->V : std::min<int64_t>(h->V, std::max<int64_t>(hot, l2_rows));
     if (h->knobs.sn_coherent_rows >= 0) a.hot_wc = std::min<int64_t>(h->V, h->knobs.sn_coherent_rows);  // experiments
     a.hot_atomic = h->sched == W2V_SCHED_PARALLEL ? hot : 0;
     if (h->knobs.sn_atomic_rows >= 0) a.hot_atomic = std::min<int64_t>(h->V, h->knobs.sn_atomic_rows);  // experiments
-    priv_scales(h, a, g, true);
+    priv_scales(h, a, h->knobs.scale_resident ? g_res : g, true);
     h->last_hot_rows = a.hot_atomic;
     h->last_hot_nodes = 0;
     h->last_priv = a.priv_n;
@@ -907,12 +1077,15 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   KernelFn fn = kernel_for(h);
   HIP_TRY(hipMemsetAsync(h->work, 0, sizeof(unsigned int), h->stream));
   dim3 grid(1), block(64);
+  int64_t resident_waves = 1, resident_wg = 1;
   if (h->sched == W2V_SCHED_PARALLEL) {
     const int threads = wpb * w2v::kWave;
     int per_cu = 0;
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds_bytes));
     if (per_cu < 1) per_cu = 1;
     const int64_t resident = (int64_t)per_cu * h->n_cu;
+    resident_waves = (int64_t)per_cu * h->n_cu * (max_wpb);
+    resident_wg = resident;
     const int64_t need = (count + wpb - 1) / wpb;
     int64_t g = need < resident ? need : resident;
     if (h->max_waves > 0 && (h->max_waves + wpb - 1) / wpb < g) g = (h->max_waves + wpb - 1) / wpb;
@@ -921,7 +1094,12 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     block = dim3(threads);
   }
   {
-    const std::pair<int64_t, int64_t> hot = hot_for((double)grid.x * (block.x / w2v::kWave), false);
+    // The rule counts every wave the chip could run, not this launch's grid:
+    // a small launch (a round's slice, a wave cap) still spreads over the XCDs,
+    // whose L2s keep stale copies of the rows they read however few waves run
+    // (measured: two replicas on one GPU trained in 1/8-epoch slices collapsed
+    // to analogy 3 with the launch-grid count; tests/test_gpu_replicas.py).
+    const std::pair<int64_t, int64_t> hot = hot_for((double)resident_waves, false);
     a.hot_wc = hot.first;
     a.hot_s = (h->V - 1) - hot.second;  // the `nodes` internal nodes nearest the root (the root is V-2)
     h->last_hot_rows = hot.first;
@@ -958,13 +1136,19 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
       }
     }
   }
-  priv_scales(h, a, grid.x, false);
+  // Flush scales from the launch's own grid (the workgroups that actually
+  // race). Counting the chip's resident workgroups instead (W2V_SCALE_RESIDENT)
+  // helps small launches (CBOW-HS in 16 slices per epoch, text8-like: analogy
+  // 24.5 vs 12.2) but over-damps a corpus with fewer sentences than the chip
+  // holds waves (planted CBOW-HS: similarity -13 vs the oracle; profiles/r02l_*, r02r_*).
+  priv_scales(h, a, h->knobs.scale_resident ? resident_wg : (int64_t)grid.x, false);
   hipLaunchKernelGGL(fn, grid, block, lds_bytes, h->stream, a);
   HIP_TRY(hipGetLastError());
   return W2V_OK;
 }
 
 int w2v_dev_train_epoch(w2v_dev* h, int32_t epoch, const int64_t* order, w2v_dev_stats* st) {
+  w2v::Range range_("w2v_dev_train_epoch");
   if (!h) return fail(W2V_ERR_ARG, "null handle");
   w2v_dev_stats before{};
   {
@@ -978,6 +1162,7 @@ int w2v_dev_train_epoch(w2v_dev* h, int32_t epoch, const int64_t* order, w2v_dev
     if (set_device(h)) return W2V_ERR_HIP;
     HIP_TRY(hipMemcpyAsync(h->order, order, h->n_sent * sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
     od = h->order;
+    h->n_order = h->n_sent;
   }
   int rc = w2v_dev_train_epoch_async(h, epoch, od);
   if (rc) return rc;
@@ -1002,6 +1187,7 @@ int w2v_dev_train_epoch(w2v_dev* h, int32_t epoch, const int64_t* order, w2v_dev
 }
 
 int w2v_dev_synchronize(w2v_dev* h) {
+  w2v::Range range_("w2v_dev_synchronize");
   if (!h) return fail(W2V_ERR_ARG, "null handle");
   if (set_device(h)) return W2V_ERR_HIP;
   HIP_TRY(hipStreamSynchronize(h->stream));
@@ -1077,6 +1263,13 @@ int w2v_dev_set_hot_rows(w2v_dev* h, int64_t hot_rows) {
   if (!h) return fail(W2V_ERR_ARG, "null handle");
   if (hot_rows < W2V_HOT_AUTO) return fail(W2V_ERR_ARG, "hot_rows must be >= -2 (W2V_HOT_AUTO)");
   h->hot_rows = hot_rows;
+  return W2V_OK;
+}
+
+int w2v_dev_set_private_rate(w2v_dev* h, float mu) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (!(mu >= 0.0f)) return fail(W2V_ERR_ARG, "private_rate must be >= 0");
+  h->private_rate = mu;
   return W2V_OK;
 }
 

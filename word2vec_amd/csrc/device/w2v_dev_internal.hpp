@@ -1,0 +1,33 @@
+// w2v_dev_internal.hpp — what the C-ABI's translation units share (not part of
+// the public boundary, include/w2v_dev.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
+
+#include <cstdint>
+#include <string>
+
+#include "w2v_dev.h"
+
+namespace w2v {
+
+// Record `msg` as this thread's w2v_dev_last_error(); returns `code`.
+int set_error(int code, const std::string& msg);
+
+struct DevInfo {
+  int device;
+  hipStream_t stream;
+  int64_t V;
+};
+DevInfo dev_info(const w2v_dev* h);
+
+// roctx range for the duration of a scope (rocprofv3 --marker-trace shows the
+// C-ABI's uploads, epochs and replica exchanges on the timeline).
+struct Range {
+  explicit Range(const char* name) { roctxRangePushA(name); }
+  ~Range() { roctxRangePop(); }
+  Range(const Range&) = delete;
+  Range& operator=(const Range&) = delete;
+};
+
+}  // namespace w2v

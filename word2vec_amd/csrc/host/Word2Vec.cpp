@@ -259,6 +259,13 @@ void Word2Vec::ensure_device() {
 
 void Word2Vec::upload_vocab_products() {
   if (!dev_vocab_stale_) return;
+  upload_vocab_to(dev_);
+  dev_vocab_stale_ = false;
+}
+
+// The vocab products the kernels read (sample probabilities, table
+// boundaries, Huffman CSR) onto one device handle.
+void Word2Vec::upload_vocab_to(w2v_dev* d) {
   const int64_t V = (int64_t)vocab.size();
   std::vector<float> keep((size_t)V);
   std::vector<int64_t> counts((size_t)V);
@@ -286,11 +293,21 @@ void Word2Vec::upload_vocab_products() {
     }
     if (codes.empty()) { codes.push_back(0); points.push_back(0); }
   }
-  check(w2v_dev_upload_vocab(dev_, V, keep.data(), bounds.empty() ? nullptr : bounds.data(),
+  check(w2v_dev_upload_vocab(d, V, keep.data(), bounds.empty() ? nullptr : bounds.data(),
                              codes.empty() ? nullptr : codes.data(), points.empty() ? nullptr : points.data(),
                              off.empty() ? nullptr : off.data()),
         "w2v_dev_upload_vocab");
-  dev_vocab_stale_ = false;
+}
+
+void Word2Vec::apply_policy(w2v_dev* d) {
+  check(w2v_dev_set_fixed_alpha(d, 0.0f), "w2v_dev_set_fixed_alpha");
+  check(w2v_dev_set_hot_rows(d, hot_rows), "w2v_dev_set_hot_rows");
+  check(w2v_dev_set_private_rows(d, private_rows), "w2v_dev_set_private_rows");
+  check(w2v_dev_set_private_sync(d, flush_centers, private_average), "w2v_dev_set_private_sync");
+  check(w2v_dev_set_max_waves(d, max_waves), "w2v_dev_set_max_waves");
+  check(w2v_dev_set_context_private(d, context_rows, context_flush), "w2v_dev_set_context_private");
+  check(w2v_dev_set_update(d, shared_negatives ? W2V_UPDATE_SHARED_NEGATIVES : W2V_UPDATE_PER_PAIR),
+        "w2v_dev_set_update");
 }
 
 // The draws the reference makes for one pass over `order`, in its order
@@ -298,7 +315,12 @@ void Word2Vec::upload_vocab_products() {
 // object's generator, with each sentence's start recorded.
 void Word2Vec::append_reference_draws(const std::vector<int32_t>& ids, const std::vector<int64_t>& offsets,
                                       const std::vector<long>& order, std::vector<uint32_t>& stream,
-                                      std::vector<int64_t>& stream_off, int64_t epoch) {
+                                      std::vector<int64_t>& stream_off, int64_t epoch, std::vector<int32_t>* negs) {
+  auto table_draw = [&]() {
+    const int pos = distribution_table(generator);
+    stream.push_back((uint32_t)pos);
+    if (negs) negs->push_back((int32_t)table[(size_t)pos]);
+  };
   const int64_t n = (int64_t)offsets.size() - 1;
   const bool cbow = model == "cbow";
   for (long s : order) {
@@ -316,11 +338,11 @@ void Word2Vec::append_reference_draws(const std::vector<int32_t>& ids, const std
       const int lo = std::max(0, i - window + rw), hi = std::min(len, i + window + 1 - rw);
       if (cbow) {
         if (hi - lo - 1 <= 0) continue;
-        for (int k = 0; k < negative; ++k) stream.push_back((uint32_t)distribution_table(generator));
+        for (int k = 0; k < negative; ++k) table_draw();
       } else {
         for (int j = lo; j < hi; ++j) {
           if (j == i) continue;
-          for (int k = 0; k < negative; ++k) stream.push_back((uint32_t)distribution_table(generator));
+          for (int k = 0; k < negative; ++k) table_draw();
         }
       }
     }
@@ -330,6 +352,10 @@ void Word2Vec::append_reference_draws(const std::vector<int32_t>& ids, const std
 // The epoch loop of Word2Vec.cpp:367-395 with the model resident in HBM.
 void Word2Vec::run_epochs(const std::vector<int32_t>& ids, const std::vector<int64_t>& offsets,
                           int64_t train_words) {
+  if (gpu_devices.size() > 1) {
+    run_epochs_replicas(ids, offsets, train_words);
+    return;
+  }
   ensure_device();
   upload_vocab_products();
   check(w2v_dev_upload_model(dev_, W.data(), uses_C() ? C.data() : nullptr,
@@ -338,15 +364,8 @@ void Word2Vec::run_epochs(const std::vector<int32_t>& ids, const std::vector<int
   const int64_t n = (int64_t)offsets.size() - 1;
   check(w2v_dev_upload_corpus(dev_, ids.data(), (int64_t)ids.size(), offsets.data(), n, train_words),
         "w2v_dev_upload_corpus");
-  check(w2v_dev_set_fixed_alpha(dev_, 0.0f), "w2v_dev_set_fixed_alpha");
-  check(w2v_dev_set_hot_rows(dev_, hot_rows), "w2v_dev_set_hot_rows");
-  check(w2v_dev_set_private_rows(dev_, private_rows), "w2v_dev_set_private_rows");
-  check(w2v_dev_set_private_sync(dev_, flush_centers, private_average), "w2v_dev_set_private_sync");
-  check(w2v_dev_set_max_waves(dev_, max_waves), "w2v_dev_set_max_waves");
-  check(w2v_dev_set_context_private(dev_, context_rows, context_flush), "w2v_dev_set_context_private");
-  check(w2v_dev_set_update(dev_, shared_negatives ? W2V_UPDATE_SHARED_NEGATIVES : W2V_UPDATE_PER_PAIR),
-        "w2v_dev_set_update");
-  check(w2v_dev_set_progress(dev_, 0), "w2v_dev_set_progress");  // current_words = 0 (:359)
+  apply_policy(dev_);
+  check(w2v_dev_set_progress(dev_, resume_ ? start_words_ : 0), "w2v_dev_set_progress");  // current_words = 0 (:359)
   std::vector<long> sample_idx((size_t)n);
   std::iota(sample_idx.begin(), sample_idx.end(), 0);
   std::vector<std::vector<int64_t>> orders;
@@ -386,15 +405,125 @@ void Word2Vec::run_epochs(const std::vector<int32_t>& ids, const std::vector<int
   int64_t cw = 0;
   check(w2v_dev_get_progress(dev_, &cw), "w2v_dev_get_progress");
   cur_words_ = cw;
+  resume_ = false;
   check(w2v_dev_download_model(dev_, W.data(), uses_C() ? C.data() : nullptr,
                                train_method == "hs" ? synapses1.data() : nullptr),
         "w2v_dev_download_model");
   if (verbose) std::printf("\n");
 }
 
+// The epoch loop of Word2Vec.cpp:367-395 over R data-parallel replicas
+// (gpu_devices): every epoch's std::shuffle order is cut into R contiguous
+// shards; each replica trains its shard in rounds and the replicas exchange
+// their updates after every round (w2v_group_average_async: summed with RCCL
+// over xGMI, or by a kernel for replicas sharing a device). The alpha schedule stays the global
+// one: each replica's counter starts a round at (global words) / R with
+// train_words / R as the denominator. Throughput mode (Philox) only.
+void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::vector<int64_t>& offsets,
+                                   int64_t train_words) {
+  if (replay_rng) throw std::runtime_error("word2vec_amd: replay_rng trains on one device (gpu_devices must be empty)");
+  const size_t R = gpu_devices.size();
+  const int64_t n = (int64_t)offsets.size() - 1;
+  w2v_dev_config cfg;
+  std::memset(&cfg, 0, sizeof(cfg));
+  cfg.word_dim = word_dim;
+  cfg.window = window;
+  cfg.negative = negative;
+  cfg.hs = train_method == "hs" ? 1 : 0;
+  cfg.cbow = model == "cbow" ? 1 : 0;
+  cfg.cbow_mean = cbow_mean ? 1 : 0;
+  cfg.iter = iter;
+  cfg.init_alpha = init_alpha;
+  cfg.min_alpha = min_alpha;
+  cfg.table_size = table_size;
+  std::vector<w2v_dev*> reps(R, nullptr);
+  w2v_group* grp = nullptr;
+  auto release = [&]() {
+    if (grp) w2v_group_destroy(grp);
+    grp = nullptr;
+    for (auto*& r : reps) {
+      if (r) w2v_dev_destroy(r);
+      r = nullptr;
+    }
+  };
+  try {
+    const uint64_t key = ((uint64_t)generator() << 32) | (uint64_t)generator();
+    for (size_t i = 0; i < R; ++i) {
+      cfg.device = gpu_devices[i];
+      check(w2v_dev_create(&cfg, &reps[i]), "w2v_dev_create");
+      upload_vocab_to(reps[i]);
+      check(w2v_dev_upload_model(reps[i], W.data(), uses_C() ? C.data() : nullptr,
+                                 train_method == "hs" ? synapses1.data() : nullptr),
+            "w2v_dev_upload_model");
+      check(w2v_dev_upload_corpus(reps[i], ids.data(), (int64_t)ids.size(), offsets.data(), n,
+                                  std::max<int64_t>(1, train_words)),
+            "w2v_dev_upload_corpus");
+      check(w2v_dev_set_train_words(reps[i], std::max<int64_t>(1, train_words / (int64_t)R)),
+            "w2v_dev_set_train_words");
+      apply_policy(reps[i]);
+      check(w2v_dev_set_rng(reps[i], W2V_RNG_PHILOX, key), "w2v_dev_set_rng");
+      check(w2v_dev_set_schedule(reps[i], W2V_SCHED_PARALLEL), "w2v_dev_set_schedule");
+    }
+    check(w2v_group_create(reps.data(), (int32_t)R, nullptr, (int32_t)R, 0, &grp), "w2v_group_create");
+    check(w2v_group_set_overlap(grp, overlap_average ? 1 : 0), "w2v_group_set_overlap");
+    check(w2v_group_set_mode(grp, replica_mode), "w2v_group_set_mode");
+    std::vector<long> sample_idx((size_t)n);
+    std::iota(sample_idx.begin(), sample_idx.end(), 0);
+    int64_t global = resume_ ? start_words_ : 0;  // the reference's current_words over all replicas (:359, :393)
+    for (int it = 0; it < iter; ++it) {
+      std::shuffle(sample_idx.begin(), sample_idx.end(), generator);  // :373
+      // shards and their per-sentence word counts
+      std::vector<std::vector<int64_t>> shard(R), cum(R);
+      int64_t largest = 0;
+      for (size_t i = 0; i < R; ++i) {
+        const int64_t lo = n * (int64_t)i / (int64_t)R, hi = n * (int64_t)(i + 1) / (int64_t)R;
+        shard[i].assign(sample_idx.begin() + lo, sample_idx.begin() + hi);
+        cum[i].assign(1, 0);
+        for (int64_t s2 : shard[i]) cum[i].push_back(cum[i].back() + offsets[(size_t)s2 + 1] - offsets[(size_t)s2]);
+        largest = std::max(largest, cum[i].back());
+        check(w2v_dev_set_order(reps[i], shard[i].data(), (int64_t)shard[i].size()), "w2v_dev_set_order");
+      }
+      const int64_t rounds = sync_words > 0 ? std::max<int64_t>(1, (largest + sync_words - 1) / sync_words) : 1;
+      for (int64_t r = 0; r < rounds; ++r) {
+        int64_t words = 0;
+        for (size_t i = 0; i < R; ++i) {
+          const int64_t m = (int64_t)shard[i].size(), lo = m * r / rounds, hi = m * (r + 1) / rounds;
+          check(w2v_dev_set_progress_async(reps[i], global / (int64_t)R), "w2v_dev_set_progress_async");
+          if (hi > lo) check(w2v_dev_train_slice_async(reps[i], it, lo, hi - lo), "w2v_dev_train_slice_async");
+          words += cum[i][(size_t)hi] - cum[i][(size_t)lo];
+        }
+        check(w2v_group_average_async(grp), "w2v_group_average_async");
+        global += words;
+      }
+      check(w2v_group_finish(grp), "w2v_group_finish");
+      for (size_t i = 0; i < R; ++i) {
+        w2v_dev_stats st;
+        check(w2v_dev_read_stats(reps[i], &st), "w2v_dev_read_stats");
+        if (st.nonfinite > 0)
+          throw std::runtime_error("word2vec_amd: training diverged on replica " + std::to_string(i) + " (" +
+                                   std::to_string(st.nonfinite) + " non-finite sigma arguments)");
+      }
+      if (verbose) {
+        std::printf("\rinit_alpha: %f  Progress: %f%% ", init_alpha, 100.0 / iter * global / train_words);
+        std::fflush(stdout);
+      }
+    }
+    cur_words_ = global;
+    resume_ = false;
+    check(w2v_dev_download_model(reps[0], W.data(), uses_C() ? C.data() : nullptr,
+                                 train_method == "hs" ? synapses1.data() : nullptr),
+          "w2v_dev_download_model");
+    if (verbose) std::printf("\n");
+  } catch (...) {
+    release();
+    throw;
+  }
+  release();
+}
+
 // Word2Vec.cpp:356-396.
 void Word2Vec::train(std::vector<std::vector<std::string>>& sentences) {
-  init_weights(vocab.size());
+  if (!resume_) init_weights(vocab.size());
   int64_t train_words = 0;
   for (auto& s : sentences) train_words += (int64_t)s.size();
   std::vector<int32_t> ids;
@@ -411,7 +540,7 @@ void Word2Vec::train(std::vector<std::vector<std::string>>& sentences) {
 
 void Word2Vec::train_ids(const std::vector<int32_t>& ids, const std::vector<int64_t>& offsets,
                          int64_t train_words) {
-  init_weights(vocab.size());
+  if (!resume_) init_weights(vocab.size());
   run_epochs(ids, offsets, train_words);
 }
 
@@ -458,7 +587,11 @@ RowVectorXf& Word2Vec::negative_sampling(Word* predict_word, RowVectorXf& projec
 
 // Word2Vec.cpp:273-317 and :319-353 on one sentence: the reference's draws for
 // it come from this object's generator (same order), the update runs on the
-// device with the caller's alpha.
+// device with the caller's alpha. Only the rows the update can touch cross
+// PCIe (the model stays resident between calls): W and C rows of the
+// sentence's words and of its negatives, and the synapses1 rows on the
+// sentence words' Huffman paths — O(touched rows x dim) per call, as the
+// reference's own update, instead of the whole V x dim model.
 void Word2Vec::train_one_sentence(std::vector<Word*>& sentence, float alpha, bool cbow) {
   const std::string saved = model;
   model = cbow ? "cbow" : "sg";
@@ -468,15 +601,41 @@ void Word2Vec::train_one_sentence(std::vector<Word*>& sentence, float alpha, boo
     std::vector<int64_t> off{0, (int64_t)ids.size()};
     ensure_device();
     upload_vocab_products();
-    check(w2v_dev_upload_model(dev_, W.data(), uses_C() && C.size() ? C.data() : nullptr,
-                               train_method == "hs" ? synapses1.data() : nullptr),
-          "w2v_dev_upload_model");
+    std::vector<uint32_t> stream;
+    std::vector<int64_t> soff(1, 0);
+    std::vector<int32_t> negs;
+    append_reference_draws(ids, off, std::vector<long>{0}, stream, soff, 0, &negs);
+    // the touched rows, sorted and unique
+    std::vector<int32_t> wc(ids);
+    wc.insert(wc.end(), negs.begin(), negs.end());
+    std::sort(wc.begin(), wc.end());
+    wc.erase(std::unique(wc.begin(), wc.end()), wc.end());
+    std::vector<int32_t> nodes;
+    if (train_method == "hs") {
+      for (int32_t w : ids)
+        for (size_t p : vocab[(size_t)w]->points) nodes.push_back((int32_t)p);
+      std::sort(nodes.begin(), nodes.end());
+      nodes.erase(std::unique(nodes.begin(), nodes.end()), nodes.end());
+    }
+    const bool has_c = uses_C() && C.size() > 0;
+    const size_t d = (size_t)word_dim;
+    std::vector<float> buf(std::max(wc.size(), nodes.size()) * d);
+    auto move_rows = [&](int which, RMatrixXf& M, const std::vector<int32_t>& rows, bool up) {
+      if (rows.empty()) return;
+      if (up)
+        for (size_t k = 0; k < rows.size(); ++k) std::memcpy(&buf[k * d], M.row((w2v_dense::Index)rows[k]).data(), d * 4);
+      check(up ? w2v_dev_upload_rows(dev_, which, rows.data(), (int64_t)rows.size(), buf.data())
+               : w2v_dev_download_rows(dev_, which, rows.data(), (int64_t)rows.size(), buf.data()),
+            up ? "w2v_dev_upload_rows" : "w2v_dev_download_rows");
+      if (!up)
+        for (size_t k = 0; k < rows.size(); ++k) std::memcpy(M.row((w2v_dense::Index)rows[k]).data(), &buf[k * d], d * 4);
+    };
+    move_rows(0, W, wc, true);
+    if (has_c) move_rows(1, C, wc, true);
+    if (train_method == "hs") move_rows(2, synapses1, nodes, true);
     check(w2v_dev_upload_corpus(dev_, ids.data(), (int64_t)ids.size(), off.data(), 1,
                                 std::max<int64_t>(1, (int64_t)ids.size())),
           "w2v_dev_upload_corpus");
-    std::vector<uint32_t> stream;
-    std::vector<int64_t> soff(1, 0);
-    append_reference_draws(ids, off, std::vector<long>{0}, stream, soff, 0);
     check(w2v_dev_upload_replay(dev_, stream.data(), (int64_t)stream.size(), soff.data(), 1),
           "w2v_dev_upload_replay");
     check(w2v_dev_set_rng(dev_, W2V_RNG_REPLAY, 0), "w2v_dev_set_rng");
@@ -484,9 +643,9 @@ void Word2Vec::train_one_sentence(std::vector<Word*>& sentence, float alpha, boo
     check(w2v_dev_set_fixed_alpha(dev_, alpha), "w2v_dev_set_fixed_alpha");
     check(w2v_dev_train_epoch(dev_, 0, nullptr, nullptr), "w2v_dev_train_epoch");
     check(w2v_dev_set_fixed_alpha(dev_, 0.0f), "w2v_dev_set_fixed_alpha");
-    check(w2v_dev_download_model(dev_, W.data(), uses_C() && C.size() ? C.data() : nullptr,
-                                 train_method == "hs" ? synapses1.data() : nullptr),
-          "w2v_dev_download_model");
+    move_rows(0, W, wc, false);
+    if (has_c) move_rows(1, C, wc, false);
+    if (train_method == "hs") move_rows(2, synapses1, nodes, false);
   } catch (...) {
     model = saved;
     throw;
@@ -570,4 +729,97 @@ void Word2Vec::load_word2vec(std::string filename, bool binary) {
       for (size_t i = 0; i < dim && (RMatrixXf::Index)i < row.size(); ++i) iss >> row[(RMatrixXf::Index)i];
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Checkpoints (additive; SURVEY.md §5: the reference saves only the final
+// vectors, Word2Vec.cpp:398-438). A snapshot between train() calls: W, C,
+// synapses1, the word counter (current_words, Word2Vec.cpp:359,393) and the
+// generator state, with the vocabulary's size and a hash of its words to catch
+// a mismatched resume. load_checkpoint restores them; the next train() /
+// train_ids() / train_file() then continues from the restored weights (no
+// init_weights) with current_words starting at the saved count.
+// ---------------------------------------------------------------------------
+namespace {
+
+const char kCkptMagic[8] = {'W', '2', 'V', 'C', 'K', 'P', 'T', '1'};
+
+uint64_t vocab_hash64(const std::vector<Word*>& vocab) {
+  uint64_t h = 1469598103934665603ull;  // FNV-1a over "text\0count\0" in vocab order
+  for (const Word* w : vocab) {
+    for (char c : w->text + std::string(1, '\0') + std::to_string(w->count) + std::string(1, '\0')) {
+      h ^= (uint8_t)c;
+      h *= 1099511628211ull;
+    }
+  }
+  return h;
+}
+
+void write_matrix(std::ofstream& out, const RMatrixXf& M) {
+  const int64_t r = M.rows(), c = M.cols();
+  out.write((const char*)&r, 8);
+  out.write((const char*)&c, 8);
+  if (r * c > 0) out.write((const char*)M.data(), (std::streamsize)(r * c * 4));
+}
+
+void read_matrix(std::ifstream& in, RMatrixXf& M) {
+  int64_t r = 0, c = 0;
+  in.read((char*)&r, 8);
+  in.read((char*)&c, 8);
+  if (!in || r < 0 || c < 0 || r * c > ((int64_t)1 << 40)) throw std::runtime_error("checkpoint: bad matrix header");
+  M.resize((w2v_dense::Index)r, (w2v_dense::Index)c);
+  if (r * c > 0) in.read((char*)M.data(), (std::streamsize)(r * c * 4));
+  if (!in) throw std::runtime_error("checkpoint: truncated matrix");
+}
+
+}  // namespace
+
+void Word2Vec::save_checkpoint(const std::string& path) {
+  std::ofstream out(path, std::ios::binary);
+  if (!out) throw std::runtime_error("checkpoint: cannot write " + path);
+  out.write(kCkptMagic, 8);
+  const int64_t V = (int64_t)vocab.size(), d = word_dim, cw = cur_words_;
+  const uint64_t vh = vocab_hash64(vocab);
+  out.write((const char*)&V, 8);
+  out.write((const char*)&d, 8);
+  out.write((const char*)&vh, 8);
+  out.write((const char*)&cw, 8);
+  std::ostringstream gs;
+  gs << generator;
+  const std::string g = gs.str();
+  const int64_t gl = (int64_t)g.size();
+  out.write((const char*)&gl, 8);
+  out.write(g.data(), (std::streamsize)gl);
+  write_matrix(out, W);
+  write_matrix(out, C);
+  write_matrix(out, synapses1);
+  if (!out) throw std::runtime_error("checkpoint: write failed for " + path);
+}
+
+void Word2Vec::load_checkpoint(const std::string& path) {
+  std::ifstream in(path, std::ios::binary);
+  if (!in) throw std::runtime_error("checkpoint: cannot read " + path);
+  char magic[8];
+  in.read(magic, 8);
+  if (!in || std::memcmp(magic, kCkptMagic, 8) != 0) throw std::runtime_error("checkpoint: not a word2vec_amd checkpoint");
+  int64_t V = 0, d = 0, cw = 0, gl = 0;
+  uint64_t vh = 0;
+  in.read((char*)&V, 8);
+  in.read((char*)&d, 8);
+  in.read((char*)&vh, 8);
+  in.read((char*)&cw, 8);
+  in.read((char*)&gl, 8);
+  if (!in || V != (int64_t)vocab.size() || d != word_dim || vh != vocab_hash64(vocab))
+    throw std::runtime_error("checkpoint: vocabulary or word_dim differs from this object's");
+  if (gl < 0 || gl > (1 << 20)) throw std::runtime_error("checkpoint: bad generator state");
+  std::string g((size_t)gl, '\0');
+  in.read(&g[0], (std::streamsize)gl);
+  std::istringstream gs(g);
+  gs >> generator;
+  read_matrix(in, W);
+  read_matrix(in, C);
+  read_matrix(in, synapses1);
+  cur_words_ = cw;
+  start_words_ = cw;
+  resume_ = true;
 }

@@ -6,7 +6,8 @@
 // because cbow_mean is hard-wired true (:117,180-181), min_alpha derived from
 // the pre-override 0.025 (:116), 1000-token sentences (:66), and which matrix
 // is written (:196-201). Additive: -train is honoured (the reference always
-// reads ./text8), -binary, -gpu, -replay, -shared-negatives.
+// reads ./text8), -binary, -gpu, -replay, -shared-negatives, and the
+// multi-GPU flags -gpus, -sync-words, -overlap (Word2Vec::gpu_devices).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -38,7 +39,10 @@ void usage() {
                "  -binary <0|1>         write vectors in the binary layout (default 0)\n"
                "  -gpu <int>            HIP device (default 0)\n"
                "  -replay <0|1>         reference-exact deterministic RNG replay on one wavefront\n"
-               "  -shared-negatives <0|1> skip-gram NS as the shared-negatives minibatch on the matrix cores\n\n"
+               "  -shared-negatives <0|1> skip-gram NS as the shared-negatives minibatch on the matrix cores\n"
+               "  -gpus <int>           data-parallel replicas on devices gpu .. gpu+n-1, averaged with RCCL (default 1)\n"
+               "  -sync-words <int>     average the replicas every this many words of a shard (default 0: per epoch)\n"
+               "  -overlap <0|1>        overlap the averaging with the next round's training (default 1)\n\n"
                "example: ./word2vec -train text8 -output vec.txt -size 300 -window 5 -subsample 1e-4 "
                "-negative 5 -model sg -train_method ns -iter 3\n";
 }
@@ -68,7 +72,8 @@ int main(int argc, char** argv) {
   float init_alpha = 0.025f, subsample_threshold = 0.0001f;
   const float min_alpha = init_alpha * 0.0001;
   const bool cbow_mean = true;
-  int binary = 0, gpu = 0, replay = 0, shared = 0;
+  int binary = 0, gpu = 0, replay = 0, shared = 0, gpus = 1, overlap = 1;
+  long long sync_words = 0;
   int i;
   if ((i = find_flag("-size", argc, argv)) > 0) word_dim = std::atoi(argv[i + 1]);
   if ((i = find_flag("-train", argc, argv)) > 0) input_file = argv[i + 1];
@@ -88,6 +93,13 @@ int main(int argc, char** argv) {
   if ((i = find_flag("-gpu", argc, argv)) > 0) gpu = std::atoi(argv[i + 1]);
   if ((i = find_flag("-replay", argc, argv)) > 0) replay = std::atoi(argv[i + 1]);
   if ((i = find_flag("-shared-negatives", argc, argv)) > 0) shared = std::atoi(argv[i + 1]);
+  if ((i = find_flag("-gpus", argc, argv)) > 0) gpus = std::atoi(argv[i + 1]);
+  if ((i = find_flag("-sync-words", argc, argv)) > 0) sync_words = std::atoll(argv[i + 1]);
+  if ((i = find_flag("-overlap", argc, argv)) > 0) overlap = std::atoi(argv[i + 1]);
+  if (gpus < 1 || sync_words < 0) {
+    std::cout << "Please set -gpus >= 1 and -sync-words >= 0!" << std::endl;
+    return 1;
+  }
 
   if (model.empty()) {
     model = "sg";
@@ -116,6 +128,10 @@ int main(int argc, char** argv) {
   w2v.gpu_device = gpu;
   w2v.replay_rng = replay != 0;
   w2v.shared_negatives = shared != 0;
+  if (gpus > 1)
+    for (int k = 0; k < gpus; ++k) w2v.gpu_devices.push_back(gpu + k);
+  w2v.sync_words = sync_words;
+  w2v.overlap_average = overlap != 0;
   // main.cpp:63-92's reader (1000-token sentences), streamed from the mapped
   // file by host threads: the same vocabulary and samples as building
   // vector<vector<string>> first (Word2Vec::build_vocab_file / train_file)

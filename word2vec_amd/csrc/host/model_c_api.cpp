@@ -96,6 +96,12 @@ void w2v_model_context_policy(w2v_model* m, int32_t context_rows, int32_t contex
 
 void w2v_model_set_shared_negatives(w2v_model* m, int32_t on) { m->w.shared_negatives = on != 0; }
 
+void w2v_model_replicas(w2v_model* m, const int32_t* devices, int32_t n, int64_t sync_words, int32_t overlap) {
+  m->w.gpu_devices.assign(devices, devices + (n > 0 && devices ? n : 0));
+  m->w.sync_words = sync_words;
+  m->w.overlap_average = overlap != 0;
+}
+
 int w2v_model_build_vocab(w2v_model* m, const char* text, int64_t len) {
   return guard(m, [&] {
     auto s = parse(text, len);
@@ -242,6 +248,13 @@ int w2v_model_save(w2v_model* m, const char* path, int32_t which, int32_t binary
 int w2v_model_load(w2v_model* m, const char* path, int32_t binary) {
   return guard(m, [&] { m->w.load_word2vec(path, binary != 0); });
 }
+int w2v_model_save_checkpoint(w2v_model* m, const char* path) {
+  return guard(m, [&] { m->w.save_checkpoint(path); });
+}
+int w2v_model_load_checkpoint(w2v_model* m, const char* path) {
+  return guard(m, [&] { m->w.load_checkpoint(path); });
+}
+int64_t w2v_model_current_words(w2v_model* m) { return m->w.current_words(); }
 int w2v_model_save_vocab(w2v_model* m, const char* path) {
   return guard(m, [&] { m->w.save_vocab(path); });
 }

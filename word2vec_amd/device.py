@@ -140,6 +140,14 @@ class DeviceTrainer:
     def set_progress(self, cw: int):
         self._chk(self.lib.w2v_dev_set_progress(self.h, int(cw)), "w2v_dev_set_progress")
 
+    def set_progress_async(self, cw: int):
+        """Set the device word counter, ordered on the handle's stream (no host sync)."""
+        self._chk(self.lib.w2v_dev_set_progress_async(self.h, int(cw)), "w2v_dev_set_progress_async")
+
+    def set_train_words(self, train_words: int):
+        """Denominator of the alpha schedule (Word2Vec.cpp:362-363,379-380)."""
+        self._chk(self.lib.w2v_dev_set_train_words(self.h, int(train_words)), "w2v_dev_set_train_words")
+
     def get_progress(self) -> int:
         v = C.c_int64()
         self._chk(self.lib.w2v_dev_get_progress(self.h, C.byref(v)), "w2v_dev_get_progress")
@@ -160,6 +168,16 @@ class DeviceTrainer:
         """Train `count` sentences listed in a device int64 array (a slice of an epoch's order)."""
         self._chk(self.lib.w2v_dev_train_sentences_async(self.h, int(epoch), C.c_void_p(order_dev_ptr), int(count)),
                   "w2v_dev_train_sentences_async")
+
+    def set_order(self, order):
+        """Keep an epoch's sentence order on the device (for train_slice_async)."""
+        o = np.ascontiguousarray(order, dtype=np.int64)
+        self._chk(self.lib.w2v_dev_set_order(self.h, _ptr(o), o.size), "w2v_dev_set_order")
+
+    def train_slice_async(self, epoch: int, first: int, count: int):
+        """Train order[first:first + count] of the order set with set_order."""
+        self._chk(self.lib.w2v_dev_train_slice_async(self.h, int(epoch), int(first), int(count)),
+                  "w2v_dev_train_slice_async")
 
     def synchronize(self):
         self._chk(self.lib.w2v_dev_synchronize(self.h), "w2v_dev_synchronize")
@@ -194,6 +212,10 @@ class DeviceTrainer:
     def set_private_rows(self, n: int):
         """Hottest output rows privatised per workgroup in LDS: -1 auto (default), 0 off."""
         self._chk(self.lib.w2v_dev_set_private_rows(self.h, int(n)), "w2v_dev_set_private_rows")
+
+    def set_private_rate(self, mu: float):
+        """Privatise only rows updated >= mu times per center (0 = no rate limit)."""
+        self._chk(self.lib.w2v_dev_set_private_rate(self.h, float(mu)), "w2v_dev_set_private_rate")
 
     def set_private_sync(self, flush_centers: int = 0, average_over: float = 8.0):
         """Workgroup centers between flushes of the private rows (0 = auto) and the

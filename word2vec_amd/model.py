@@ -32,6 +32,7 @@ def _load():
             "w2v_model_update_policy": (None, [P, I64, I32, I32, F, I64]),
             "w2v_model_context_policy": (None, [P, I32, I32]),
             "w2v_model_set_shared_negatives": (None, [P, I32]),
+            "w2v_model_replicas": (None, [P, P, I32, I64, I32]),
             "w2v_model_build_vocab": (C.c_int, [P, S, I64]),
             "w2v_model_train": (C.c_int, [P, S, I64]),
             "w2v_model_train_ids": (C.c_int, [P, P, P, I64, I64]),
@@ -57,6 +58,9 @@ def _load():
             "w2v_model_save": (C.c_int, [P, S, I32, I32]),
             "w2v_model_load": (C.c_int, [P, S, I32]),
             "w2v_model_save_vocab": (C.c_int, [P, S]),
+            "w2v_model_save_checkpoint": (C.c_int, [P, S]),
+            "w2v_model_load_checkpoint": (C.c_int, [P, S]),
+            "w2v_model_current_words": (I64, [P]),
             "w2v_model_read_vocab": (C.c_int, [P, S]),
         }
         for k, (r, a) in sig.items():
@@ -83,7 +87,7 @@ class Word2Vec:
                  subsample_threshold=0.001, init_alpha=0.025, min_alpha=1e-6, cbow_mean=False, num_threads=1,
                  train_method="hs", model="cbow", gpu_device=0, replay_rng=False, verbose=False, hot_rows=-2,
                  private_rows=-1, flush_centers=0, private_average=8.0, max_waves=0, shared_negatives=False,
-                 context_rows=-1, context_flush=0):
+                 context_rows=-1, context_flush=0, gpu_devices=None, sync_words=0, overlap_average=True):
         self.L = _load()
         self.word_dim = word_dim
         self.h = self.L.w2v_model_new(iter, window, min_count, table_size, word_dim, negative, subsample_threshold,
@@ -96,6 +100,9 @@ class Word2Vec:
                                        float(private_average), int(max_waves))
         self.L.w2v_model_set_shared_negatives(self.h, int(bool(shared_negatives)))
         self.L.w2v_model_context_policy(self.h, int(context_rows), int(context_flush))
+        if gpu_devices:
+            devs = np.ascontiguousarray(gpu_devices, np.int32)
+            self.L.w2v_model_replicas(self.h, _p(devs), devs.size, int(sync_words), int(bool(overlap_average)))
 
     def __del__(self):
         try:
@@ -172,6 +179,17 @@ class Word2Vec:
 
     def load_word2vec(self, path, binary=False):
         self._chk(self.L.w2v_model_load(self.h, str(path).encode(), int(binary)), "load_word2vec")
+
+    def save_checkpoint(self, path):
+        self._chk(self.L.w2v_model_save_checkpoint(self.h, str(path).encode()), "save_checkpoint")
+
+    def load_checkpoint(self, path):
+        """Restore W / C / synapses1, current_words and the generator; the next train continues from them."""
+        self._chk(self.L.w2v_model_load_checkpoint(self.h, str(path).encode()), "load_checkpoint")
+
+    @property
+    def current_words(self) -> int:
+        return self.L.w2v_model_current_words(self.h)
 
     def save_vocab(self, path):
         self._chk(self.L.w2v_model_save_vocab(self.h, str(path).encode()), "save_vocab")

@@ -5,16 +5,26 @@ The reference parallelises only with OpenMP threads sharing one model
 (torchrun), gives each rank a contiguous shard of the sentences and a full
 model replica in its HBM, trains the shard with the Hogwild kernels, and at
 the end of every round (every `sync_every` sentences of the largest shard, the
-same round count on every rank) averages the replicas with an RCCL all-reduce over xGMI
-(backend "nccl" is RCCL on ROCm). The alpha schedule follows the GLOBAL word
-count: after each averaging round the per-rank counters are summed and every
-rank resumes from the sum, with train_words the global raw-token total
-(Word2Vec.cpp:362-363,379-380).
+same round count on every rank) averages the replicas.
 
-Works unchanged on the gloo backend with CPU tensors (the CPU tests use that).
+The exchange is native: `NativeAverager` wraps the C-ABI's RCCL group
+(include/w2v_dev.h w2v_group_*: the replicas' updates since the last exchange
+summed with one ncclAllReduce per matrix over xGMI and averaged per row over
+the replicas that changed it, optionally overlapped with the next round's
+training). `TorchAverager` (model averaging
+over torch.distributed) is what the CPU tests run on the gloo backend to
+exercise the round logic, which is the same object code.
+
+The alpha schedule stays global without a collective per round: each rank
+knows every rank's words per round (exchanged once, `global_round_words`), sets
+its device counter to (global words at the round start) / world and its
+train_words to (global raw tokens) / world, so alpha follows the reference's
+schedule of the global count (Word2Vec.cpp:362-363,379-380) while the ranks
+progress in step.
 """
 from __future__ import annotations
 
+import ctypes as C
 from dataclasses import dataclass
 
 import torch
@@ -43,49 +53,117 @@ def round_slices(n: int, rounds: int) -> list[tuple[int, int]]:
     return [(n * k // rounds, n * (k + 1) // rounds) for k in range(rounds)]
 
 
+def local_round_words(sent_offsets, order, rounds: int) -> list[int]:
+    """In-vocab words of each round's slice of `order` (sentence ids into
+    sent_offsets): what the device counter advances by in that round."""
+    import numpy as np
+
+    off = np.asarray(sent_offsets, dtype=np.int64)
+    o = np.asarray(order, dtype=np.int64)
+    lens = off[o + 1] - off[o]
+    cum = np.concatenate([[0], np.cumsum(lens)])
+    return [int(cum[hi] - cum[lo]) for lo, hi in round_slices(o.size, rounds)]
+
+
+def global_round_words(local: list[int], world: int, group=None, device="cpu") -> list[int]:
+    """Sum over ranks of each round's words (one small all-reduce, once)."""
+    if world == 1:
+        return list(local)
+    t = torch.tensor(local, dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return [int(x) for x in t.cpu().tolist()]
+
+
 @dataclass
-class ReplicaGroup:
-    """The replicas of W / C / synapses1 held by this rank (torch tensors that
-    the device handle was bound to with w2v_dev_bind_model)."""
+class TorchAverager:
+    """In-place mean of this rank's replica tensors over torch.distributed
+    (the CPU tests' gloo backend; gloo has no AVG: sum then divide)."""
 
     tensors: list
     world: int
     group: object = None
 
     def average(self) -> None:
-        """In-place mean over ranks. One all-reduce per matrix: each is one
-        large contiguous buffer (V x pitch fp32), the message size RCCL's
-        ring/tree algorithms over xGMI run at full link rate."""
         if self.world == 1:
             return
         for t in self.tensors:
-            if dist.get_backend(self.group) == "nccl":
-                dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group)
-            else:  # gloo has no AVG
-                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
-                t.div_(self.world)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            t.div_(self.world)
 
-    def global_progress(self, local_words: int, device) -> int:
-        """Sum of the ranks' in-vocab word counters (the reference's current_words)."""
-        if self.world == 1:
-            return int(local_words)
-        v = torch.tensor([int(local_words)], dtype=torch.int64, device=device)
-        dist.all_reduce(v, op=dist.ReduceOp.SUM, group=self.group)
-        return int(v.item())
+    def finish(self) -> None:
+        pass
 
 
-def train_rounds(trainer, replicas: ReplicaGroup, order_dev: torch.Tensor, epoch: int, rounds: int,
-                 device, progress_base: int, events: list | None = None) -> int:
-    """One epoch of this rank's shard in rounds: train a slice of the order on
-    the device, average the replicas, move every rank to the global progress.
-    `progress_base` is the global word count at epoch start; returns the new one.
-    The kernels and the collectives are ordered on the current stream; if
-    `events` is a list, a (start, end) timing-event pair around every kernel
-    launch is appended to it."""
+class NativeAverager:
+    """The C-ABI's RCCL replica group (w2v_group_*) over this process's device
+    handles; `unique_id` (W2V_GROUP_ID_BYTES bytes from group_unique_id() on
+    rank 0) joins the handles to a multi-process group as ranks
+    [first_rank, first_rank + len(trainers)) of `nranks`."""
+
+    def __init__(self, trainers, unique_id: bytes | None = None, nranks: int | None = None, first_rank: int = 0,
+                 overlap: bool = False, mode: str = "sum"):
+        from . import _native as N
+
+        self.N = N
+        self.lib = N.load_dev_lib()
+        arr = (C.c_void_p * len(trainers))(*[t.h.value if isinstance(t.h, C.c_void_p) else t.h for t in trainers])
+        g = C.c_void_p()
+        uid = None if unique_id is None else (C.c_uint8 * N.W2V_GROUP_ID_BYTES).from_buffer_copy(unique_id)
+        N.check(self.lib, self.lib.w2v_group_create(arr, len(trainers), uid, int(nranks or len(trainers)),
+                                                    int(first_rank), C.byref(g)), "w2v_group_create")
+        self.g = g
+        self.trainers = trainers
+        N.check(self.lib, self.lib.w2v_group_set_overlap(self.g, int(bool(overlap))), "w2v_group_set_overlap")
+        modes = {"row_average": N.W2V_GROUP_ROW_AVERAGE, "sum": N.W2V_GROUP_SUM, "average": N.W2V_GROUP_AVERAGE}
+        N.check(self.lib, self.lib.w2v_group_set_mode(self.g, modes[mode]), "w2v_group_set_mode")
+
+    def average(self) -> None:
+        self.N.check(self.lib, self.lib.w2v_group_average_async(self.g), "w2v_group_average_async")
+
+    def finish(self) -> None:
+        self.N.check(self.lib, self.lib.w2v_group_finish(self.g), "w2v_group_finish")
+
+    def info(self) -> dict:
+        n, loc, ov, r = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64()
+        self.N.check(self.lib, self.lib.w2v_group_info(self.g, C.byref(n), C.byref(loc), C.byref(ov), C.byref(r)),
+                     "w2v_group_info")
+        return {"nranks": n.value, "local": bool(loc.value), "overlap": bool(ov.value), "rounds": r.value}
+
+    def close(self) -> None:
+        if getattr(self, "g", None):
+            self.lib.w2v_group_destroy(self.g)
+            self.g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def group_unique_id() -> bytes:
+    from . import _native as N
+
+    lib = N.load_dev_lib()
+    buf = (C.c_uint8 * N.W2V_GROUP_ID_BYTES)()
+    N.check(lib, lib.w2v_group_unique_id(buf), "w2v_group_unique_id")
+    return bytes(buf)
+
+
+def train_rounds(trainer, averager, order_dev: torch.Tensor, epoch: int, rounds: int, progress_base: int,
+                 round_words: list[int], world: int, events: list | None = None) -> int:
+    """One epoch of this rank's shard in `rounds` rounds, all enqueued on the
+    trainer's stream without a host sync: per round, the device counter is set
+    to (global words at the round start) / world, the slice trains, and the
+    replicas are averaged. `progress_base` is the global word count at epoch
+    start, round_words[r] the words all ranks train in round r; returns the
+    global count at epoch end. If `events` is a list, a (start, end)
+    torch.cuda.Event pair around every kernel launch is appended to it (they
+    are recorded on torch's current stream, which must be the trainer's)."""
     n = order_dev.numel()
-    global_words = progress_base
-    for lo, hi in round_slices(n, rounds):
-        trainer.set_progress(global_words)
+    g = progress_base
+    for r, (lo, hi) in enumerate(round_slices(n, rounds)):
+        trainer.set_progress_async(g // world)
         if hi > lo:
             ev = None
             if events is not None:
@@ -95,7 +173,6 @@ def train_rounds(trainer, replicas: ReplicaGroup, order_dev: torch.Tensor, epoch
             if ev is not None:
                 ev[1].record()
                 events.append(ev)
-        replicas.average()
-        local = trainer.get_progress() - global_words
-        global_words += replicas.global_progress(local, device)
-    return global_words
+        averager.average()
+        g += round_words[r]
+    return g
