@@ -1,0 +1,57 @@
+"""CPU simulation of replica exchange with the oracle (sequential per replica)."""
+import sys; sys.path.insert(0, "/root/repo")
+import numpy as np
+from tests import paired
+from word2vec_amd.evaluate import analogy_accuracy, similarity_score
+name, mode, R, rounds, how = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
+warm = float(sys.argv[6]) if len(sys.argv) > 6 else 0.0
+sents, qs, pairs = paired.corpus(name)
+o, orders, key, p = paired.setup(name, mode, 1, sents)
+ids, off = o.samples()
+n = off.size - 1
+order = orders[:n]
+words, _ = o.vocab()
+mats = [0, 1] if mode.endswith("ns") or mode.startswith("cbow") else [0]
+if mode.endswith("hs"): mats = mats + [2]
+P = {k: o.matrix(k).copy() for k in mats}
+glob = 0
+tw = o.train_words
+if warm > 0:  # replica 0 alone trains the first `warm` fraction, then the rest is sharded
+    nw = int(n * warm)
+    wl = order[:nw]
+    sub_ids = np.concatenate([ids[off[s]:off[s + 1]] for s in wl])
+    sub_off = np.concatenate([[0], np.cumsum([off[s + 1] - off[s] for s in wl])])
+    for k in mats: o.set_matrix(k, P[k])
+    o.set_samples(sub_ids, sub_off, tw)
+    o.train_philox(0, 1, np.arange(len(wl)), key + 999, 0)
+    for k in mats: P[k] = o.matrix(k).copy()
+    glob = int(sub_off[-1])
+    order = order[nw:]
+    n = len(order)
+shards = [order[n * i // R:n * (i + 1) // R] for i in range(R)]
+for r in range(rounds):
+    D = {k: np.zeros_like(P[k]) for k in mats}
+    touched = {k: np.zeros(P[k].shape[0]) for k in mats}
+    for i in range(R):
+        sh = shards[i]
+        sl = sh[len(sh) * r // rounds: len(sh) * (r + 1) // rounds]
+        # corpus = the slice's sentences (ids relabelled 0..m-1)
+        sub_ids = np.concatenate([ids[off[s]:off[s + 1]] for s in sl])
+        sub_off = np.concatenate([[0], np.cumsum([off[s + 1] - off[s] for s in sl])])
+        for k in mats: o.set_matrix(k, P[k])
+        o.set_samples(sub_ids, sub_off, max(1, tw // R))
+        o.train_philox(0, 1, np.arange(len(sl)), key + 1000 * i + r, glob // R)
+        for k in mats:
+            d = o.matrix(k) - P[k]
+            D[k] += d
+            touched[k] += (np.abs(d).max(1) > 0)
+    for k in mats:
+        if how == "sum": P[k] = P[k] + D[k]
+        elif how == "avg": P[k] = P[k] + D[k] / R
+        elif how.startswith("cap"):  # scale 1 / max(1, c / S) with S = int(how[3:])
+            S = float(how[3:])
+            P[k] = P[k] + D[k] / np.maximum(1, touched[k] / S)[:, None]
+        else: P[k] = P[k] + D[k] / np.maximum(1, touched[k])[:, None]
+    glob += sum(int(off[s + 1] - off[s]) for sh in shards for s in sh[len(sh) * r // rounds: len(sh) * (r + 1) // rounds])
+E = P[1 if mode == "cbow_hs" else 0]
+print(name, mode, R, rounds, how, warm, round(analogy_accuracy(words, E, qs)["accuracy"], 2), round(similarity_score(words, E, pairs)["spearman"], 2), flush=True)

@@ -1059,7 +1059,12 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     // per-pair kernel (parallel schedule only: the sequential one is exact
     // either way), and at least the rows two XCD L2s could keep resident are
     // device-coherent
-    const int64_t hot = hot_for((double)g_res, true).first;
+    // (automatic: at least the fixed 1000 rows of round 1 — a shared-negatives
+    // center holds its ~22 rows for its whole update, longer than a per-pair
+    // update holds one, and the rate rule alone left the text8-like gate 2.4
+    // similarity points below the oracle; profiles/r02s_gpu_tests.log)
+    int64_t hot = hot_for((double)g_res, true).first;
+    if (h->hot_rows == W2V_HOT_AUTO) hot = std::max<int64_t>(hot, std::min<int64_t>(h->V, 1000));
     a.hot_wc = h->hot_rows == -1 ? h->V : std::min<int64_t>(h->V, std::max<int64_t>(hot, l2_rows));
     if (h->knobs.sn_coherent_rows >= 0) a.hot_wc = std::min<int64_t>(h->V, h->knobs.sn_coherent_rows);  // experiments
     a.hot_atomic = h->sched == W2V_SCHED_PARALLEL ? hot : 0;
