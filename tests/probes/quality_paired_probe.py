@@ -1,7 +1,7 @@
 """GPU probe for the paired quality gates (tests/paired.py): per corpus /
 mode / seed, the GPU scores at one wavefront and at full concurrency next to
 the oracle's paired golden, with wall times. Run on the GPU box:
-python tools/quality_paired_probe.py [corpus] [modes,...] [seeds,...] [max_waves,...] [policy;policy;...]
+python tests/probes/quality_paired_probe.py [corpus] [modes,...] [seeds,...] [max_waves,...] [policy;policy;...]
 where a policy is "k=v,k=v" over tests/paired.train_gpu_paired's policy keys
 (hot_rows, private_rows, flush_centers, private_average, context_rows,
 context_flush); "-" = the default policy."""
@@ -10,7 +10,7 @@ import sys
 import time
 from pathlib import Path
 
-ROOT = Path(__file__).resolve().parents[1]
+ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT))
 
 from tests import paired  # noqa: E402

@@ -1,12 +1,12 @@
 """GPU probe: where does data-parallel replica training lose quality? Runs the
 planted corpus (tests/paired.py setup: oracle vocab, seeded init, Philox key)
 through variants of slicing and exchanging, and prints analogy / similarity.
-usage (GPU box): python tools/replica_probe.py [mode] [seed] [rounds] [corpus] [short]"""
+usage (GPU box): python tests/probes/replica_probe.py [mode] [seed] [rounds] [corpus] [short]"""
 import sys
 import time
 from pathlib import Path
 
-ROOT = Path(__file__).resolve().parents[1]
+ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT))
 
 import numpy as np  # noqa: E402

@@ -1,8 +1,8 @@
 """CPU simulation of data-parallel replica exchange with the sequential oracle per
 replica (test infrastructure: the oracle is the checker). For DESIGN.md §6 and
 profiles/r02_replica_sim_cpu.log.
-usage: python tools/replica_sim_cpu.py <corpus> <mode> <R> <rounds> <sum|avg|rowavg|capS> [warm_fraction]"""
-import sys; sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[1]))
+usage: python tests/probes/replica_sim_cpu.py <corpus> <mode> <R> <rounds> <sum|avg|rowavg|capS> [warm_fraction]"""
+import sys; sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[2]))
 import numpy as np
 from tests import paired
 from word2vec_amd.evaluate import analogy_accuracy, similarity_score

@@ -3,7 +3,7 @@
 #   bash tools/gpu_r02.sh <tag> tests [pytest -k expr]   the GPU test suite (no -x: every failure reported)
 #   bash tools/gpu_r02.sh <tag> bench                    smoke(), the headline bench line, then rocprofv3
 #                                                        kernel-trace + FETCH/WRITE passes of the same workload
-#   bash tools/gpu_r02.sh <tag> probe "<probe args>"     tools/quality_paired_probe.py
+#   bash tools/gpu_r02.sh <tag> probe "<probe args>"     tests/probes/quality_paired_probe.py
 set -o pipefail
 TAG=${1:-r02}
 PHASE=${2:-tests}
@@ -27,7 +27,7 @@ bench)
   bash tools/profile.sh ${TAG}_c3 --config c3 --steps 3 || stop profile $?
   ;;
 probe)
-  timeout -k 10 1080 python -u tools/quality_paired_probe.py $ARG > gpurun_out/${TAG}_probe.log 2>&1 || stop probe $?
+  timeout -k 10 1080 python -u tests/probes/quality_paired_probe.py $ARG > gpurun_out/${TAG}_probe.log 2>&1 || stop probe $?
   cat gpurun_out/${TAG}_probe.log
   ;;
 esac

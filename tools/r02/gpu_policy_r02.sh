@@ -12,8 +12,8 @@ for c in c3 c2 c1 c5; do
     python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], sys.argv[3], round(d['value']/1e6,2), 'M words/s', d['roofline']['frac'], d['config']['policy_used'])" gpurun_out/${TAG}_bench_${c}_hot${hr}.json $c $hr
   done
 done
-timeout -k 10 600 python -u tools/quality_paired_probe.py text8_like cbow_hs,sg_ns 1,2,3 0 "-;hot_auto=0.5;hot_auto=2;hot_rows=1000" > gpurun_out/${TAG}_probe_text8.log 2>&1 || stop probe $?
+timeout -k 10 600 python -u tests/probes/quality_paired_probe.py text8_like cbow_hs,sg_ns 1,2,3 0 "-;hot_auto=0.5;hot_auto=2;hot_rows=1000" > gpurun_out/${TAG}_probe_text8.log 2>&1 || stop probe $?
 cat gpurun_out/${TAG}_probe_text8.log
-timeout -k 10 300 python -u tools/quality_paired_probe.py planted sg_ns,sg_hs,cbow_ns,cbow_hs 1,2,3 0 "-;hot_rows=1000" > gpurun_out/${TAG}_probe_planted.log 2>&1 || stop probe2 $?
+timeout -k 10 300 python -u tests/probes/quality_paired_probe.py planted sg_ns,sg_hs,cbow_ns,cbow_hs 1,2,3 0 "-;hot_rows=1000" > gpurun_out/${TAG}_probe_planted.log 2>&1 || stop probe2 $?
 cat gpurun_out/${TAG}_probe_planted.log
 echo PHASE_DONE

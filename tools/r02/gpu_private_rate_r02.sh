@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 P="-;private_rate=0.05;private_rate=0.1;private_rate=0.2;private_rate=0.5"
 for c in text8_small planted text8_like; do
   seeds=1; [ $c = planted ] && seeds=1,2
-  timeout -k 10 400 python -u tools/quality_paired_probe.py $c sg_ns,cbow_hs $seeds 0 "$P" > gpurun_out/${TAG}_$c.log 2>&1 || { echo "probe $c failed"; tail -3 gpurun_out/${TAG}_$c.log; }
+  timeout -k 10 400 python -u tests/probes/quality_paired_probe.py $c sg_ns,cbow_hs $seeds 0 "$P" > gpurun_out/${TAG}_$c.log 2>&1 || { echo "probe $c failed"; tail -3 gpurun_out/${TAG}_$c.log; }
   cut -c1-60,100-230 gpurun_out/${TAG}_$c.log | grep corpus
 done
 for c in c3 c1 c2; do
