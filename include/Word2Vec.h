@@ -22,6 +22,7 @@
 #include "Word.h"
 #include "w2v_dense.h"
 #include "w2v_dev.h"
+#include "w2v_ingest.h"
 
 using w2v_dense::IOFormat;
 using w2v_dense::RMatrixXf;
@@ -134,6 +135,12 @@ class Word2Vec {
   // train_words as build_vocab / train on the sentences those readers return.
   void build_vocab_file(const std::string& path, const std::string& format = "lines", int threads = 0);
   void train_file(const std::string& path, const std::string& format = "lines", int threads = 0);
+  // With gpu_ingest, build_vocab_file and file_samples / train_file count and
+  // map the file on the GPU (include/w2v_ingest.h) instead of host threads:
+  // same vocabulary, ids, offsets and train_words. The count of
+  // build_vocab_file is kept for a train_file on the same file.
+  bool gpu_ingest = false;
+  int64_t ingest_chunk_bytes = 0;  // bytes per host -> device chunk (0 = 1 GiB)
   // build_sample of a corpus file as token ids (what train_file trains on).
   void file_samples(const std::string& path, const std::string& format, int threads, std::vector<int32_t>& ids,
                     std::vector<int64_t>& offsets, int64_t& train_words);
@@ -154,6 +161,11 @@ class Word2Vec {
   int64_t cur_words_ = 0;           // current_words after the last train call
   bool resume_ = false;             // load_checkpoint: the next train continues (no init_weights)
   int64_t start_words_ = 0;         //   ... from this current_words
+  w2v_ingest* ingest_ = nullptr;    // gpu_ingest: the counted file ...
+  std::string ingest_key_;          //   ... (path + format)
+  std::vector<std::string> ingest_words_;  // its distinct words, in order of first occurrence
+  std::vector<int64_t> ingest_counts_;
+  void ingest_count(const std::string& path, const std::string& format);
 
   bool uses_C() const;
   void finish_vocab(std::unordered_map<std::string, int>& tally);

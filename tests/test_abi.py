@@ -15,7 +15,8 @@ def declared(header: Path):
     return sorted(set(re.findall(r"\b(w2v_[a-z0-9_]+)\s*\(", txt)))
 
 
-@pytest.mark.parametrize("header,lib", [("w2v_dev.h", "libw2v_hip.so"), ("w2v_host.h", "libword2vec_amd.so")])
+@pytest.mark.parametrize("header,lib", [("w2v_dev.h", "libw2v_hip.so"), ("w2v_ingest.h", "libw2v_hip.so"),
+                                        ("w2v_host.h", "libword2vec_amd.so")])
 def test_library_exports_every_declared_symbol(header, lib):
     names = declared(ROOT / "include" / header)
     assert len(names) >= 4
@@ -27,7 +28,7 @@ def test_library_exports_every_declared_symbol(header, lib):
 def test_python_binding_covers_the_header():
     from word2vec_amd import _native
 
-    names = declared(ROOT / "include" / "w2v_dev.h")
+    names = sorted(set(declared(ROOT / "include" / "w2v_dev.h")) | set(declared(ROOT / "include" / "w2v_ingest.h")))
     assert sorted(_native.SIGNATURES) == names
     lib = _native.load_dev_lib()
     assert lib.w2v_dev_version().decode().startswith("word2vec_amd")
@@ -53,3 +54,16 @@ def test_create_rejects_bad_configs_without_gpu():
         cfg = N.DevConfig(**kw)
         assert lib.w2v_dev_create(ctypes.byref(cfg), ctypes.byref(h)) != 0
         assert lib.w2v_dev_last_error()
+
+
+def test_ingest_rejects_bad_arguments_without_gpu():
+    from word2vec_amd import _native as N
+
+    lib = N.load_dev_lib()
+    g = ctypes.c_void_p()
+    assert lib.w2v_ingest_create(0, 7, 0, ctypes.byref(g)) != 0  # bad format
+    assert b"format" in lib.w2v_dev_last_error()
+    assert lib.w2v_ingest_create(0, 0, -1, ctypes.byref(g)) != 0
+    assert lib.w2v_ingest_count(None, None, 0) != 0
+    assert lib.w2v_ingest_summary(None, None, None, None) != 0
+    assert lib.w2v_dev_adopt_corpus(None, None) != 0

@@ -123,7 +123,20 @@ SIGNATURES = {
     "w2v_group_average_async": (C.c_int, [_P]),
     "w2v_group_finish": (C.c_int, [_P]),
     "w2v_group_info": (C.c_int, [_P, C.POINTER(_I32), C.POINTER(_I32), C.POINTER(_I32), C.POINTER(_I64)]),
+    # include/w2v_ingest.h
+    "w2v_ingest_create": (C.c_int, [_I32, _I32, _I64, C.POINTER(_P)]),
+    "w2v_ingest_destroy": (None, [_P]),
+    "w2v_ingest_set_resident": (C.c_int, [_P, _I64]),
+    "w2v_ingest_count": (C.c_int, [_P, _P, _I64]),
+    "w2v_ingest_summary": (C.c_int, [_P, C.POINTER(_I64), C.POINTER(_I64), C.POINTER(_I64)]),
+    "w2v_ingest_words": (C.c_int, [_P, _P, _P, _P]),
+    "w2v_ingest_map": (C.c_int, [_P, _P, _I64, _P, _I64]),
+    "w2v_ingest_samples_size": (C.c_int, [_P, C.POINTER(_I64), C.POINTER(_I64), C.POINTER(_I64)]),
+    "w2v_ingest_download": (C.c_int, [_P, _P, _P]),
+    "w2v_dev_adopt_corpus": (C.c_int, [_P, _P]),
 }
+W2V_INGEST_LINES = 0
+W2V_INGEST_TEXT8 = 1
 
 _lib = None
 

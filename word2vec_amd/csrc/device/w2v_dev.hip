@@ -667,6 +667,44 @@ int w2v_dev_upload_corpus(w2v_dev* h, const int32_t* ids, int64_t n_tok, const i
   return W2V_OK;
 }
 
+int w2v_dev_adopt_corpus(w2v_dev* h, w2v_ingest* g) {
+  w2v::Range range_("w2v_dev_adopt_corpus");
+  if (!h || !g) return fail(W2V_ERR_ARG, "w2v_dev_adopt_corpus: null argument");
+  const w2v::IngestView v = w2v::ingest_view(g);
+  if (!v.ok) return fail(W2V_ERR_STATE, "w2v_dev_adopt_corpus: map the ingest first");
+  if (v.device != h->device) return fail(W2V_ERR_ARG, "w2v_dev_adopt_corpus: ingest on another device");
+  if (h->V < 1) return fail(W2V_ERR_STATE, "upload the vocab before the corpus");
+  if (v.n_vocab > h->V) return fail(W2V_ERR_ARG, "ingest vocab index beyond the handle's vocab");
+  if (v.n_sentences > (int64_t)UINT32_MAX - 1) return fail(W2V_ERR_ARG, "corpus sizes out of range");
+  if (v.train_words <= 0 && v.n_ids > 0) return fail(W2V_ERR_ARG, "train_words must be > 0");
+  if (set_device(h)) return W2V_ERR_HIP;
+  std::vector<int64_t> soff((size_t)v.n_sentences + 1);
+  HIP_TRY(hipMemcpy(soff.data(), v.offsets, soff.size() * sizeof(int64_t), hipMemcpyDeviceToHost));
+  if (soff[0] != 0 || soff.back() != v.n_ids) return fail(W2V_ERR_STATE, "ingest offsets do not span its ids");
+  int64_t max_len = 0;
+  for (int64_t s = 0; s < v.n_sentences; ++s) {
+    if (soff[s + 1] - soff[s] > (int64_t)INT32_MAX) return fail(W2V_ERR_UNSUPPORTED, "a sentence over 2^31 tokens");
+    max_len = std::max<int64_t>(max_len, soff[s + 1] - soff[s]);
+  }
+  std::vector<int64_t> hist((size_t)h->V, 0);
+  for (int64_t w = 0; w < v.n_vocab; ++w) hist[(size_t)w] = v.hist[w];
+  dfree(h->ids); dfree(h->soff); dfree(h->order);
+  HIP_TRY(hipMalloc(&h->ids, (v.n_ids > 0 ? v.n_ids : 1) * sizeof(int32_t)));
+  if (v.n_ids > 0) HIP_TRY(hipMemcpy(h->ids, v.ids, v.n_ids * sizeof(int32_t), hipMemcpyDeviceToDevice));
+  HIP_TRY(hipMalloc(&h->soff, (v.n_sentences + 1) * sizeof(int64_t)));
+  HIP_TRY(hipMemcpy(h->soff, v.offsets, (v.n_sentences + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice));
+  HIP_TRY(hipMalloc(&h->order, (v.n_sentences > 0 ? v.n_sentences : 1) * sizeof(int64_t)));
+  h->n_tok = v.n_ids;
+  h->n_sent = v.n_sentences;
+  h->n_order = 0;
+  h->max_len = max_len;
+  h->train_words = v.train_words;
+  h->tok_count.swap(hist);
+  ++h->data_version;
+  h->corpus_ready = true;
+  return W2V_OK;
+}
+
 int w2v_dev_upload_replay(w2v_dev* h, const uint32_t* stream, int64_t n, const int64_t* off,
                           int64_t n_off) {
   if (!h || !off || (n > 0 && !stream)) return fail(W2V_ERR_ARG, "w2v_dev_upload_replay: null argument");

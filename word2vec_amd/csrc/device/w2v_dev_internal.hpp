@@ -8,6 +8,7 @@
 #include <string>
 
 #include "w2v_dev.h"
+#include "w2v_ingest.h"
 
 namespace w2v {
 
@@ -20,6 +21,20 @@ struct DevInfo {
   int64_t V;
 };
 DevInfo dev_info(const w2v_dev* h);
+
+// The device samples of a mapped ingest (w2v_ingest.hip) for w2v_dev_adopt_corpus.
+struct IngestView {
+  bool ok;
+  int device;
+  const int32_t* ids;
+  int64_t n_ids;
+  const int64_t* offsets;  // n_sentences + 1
+  int64_t n_sentences;
+  int64_t train_words;
+  const int64_t* hist;  // host: tokens per vocab id, n_vocab entries
+  int64_t n_vocab;
+};
+IngestView ingest_view(const w2v_ingest* g);
 
 // roctx range for the duration of a scope (rocprofv3 --marker-trace shows the
 // C-ABI's uploads, epochs and replica exchanges on the timeline).

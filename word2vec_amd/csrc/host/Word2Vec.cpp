@@ -27,6 +27,7 @@ bool count_desc(Word* a, Word* b) { return a->count > b->count; }  // Word2Vec.c
 }  // namespace
 
 Word2Vec::~Word2Vec(void) {
+  if (ingest_) w2v_ingest_destroy(ingest_);
   if (dev_) w2v_dev_destroy(dev_);
 }
 
@@ -117,6 +118,13 @@ void Word2Vec::build_vocab(std::vector<std::vector<std::string>>& sentences) {
 // distinct words were first inserted, so a file's counts inserted in order of
 // first occurrence give the map build_vocab builds (corpus.cpp).
 void Word2Vec::build_vocab_file(const std::string& path, const std::string& format, int threads) {
+  if (gpu_ingest) {
+    ingest_count(path, format);
+    std::unordered_map<std::string, int> tally;
+    for (size_t k = 0; k < ingest_words_.size(); ++k) tally[ingest_words_[k]] = (int)ingest_counts_[k];
+    finish_vocab(tally);
+    return;
+  }
   const w2v_corpus::File f(path);
   const w2v_corpus::Counts c = w2v_corpus::count_words(f, w2v_corpus::parse_format(format), threads);
   std::unordered_map<std::string, int> tally;
@@ -124,8 +132,51 @@ void Word2Vec::build_vocab_file(const std::string& path, const std::string& form
   finish_vocab(tally);
 }
 
+// Pass 1 on the GPU (w2v_ingest_count): the distinct words in order of first
+// occurrence, their text read back from the mapped file at their first offset.
+void Word2Vec::ingest_count(const std::string& path, const std::string& format) {
+  const w2v_corpus::Format fmt = w2v_corpus::parse_format(format);
+  const std::string key = format + ":" + path;
+  if (ingest_ && ingest_key_ == key) return;
+  if (ingest_) w2v_ingest_destroy(ingest_);
+  ingest_ = nullptr;
+  ingest_key_.clear();
+  const w2v_corpus::File f(path);
+  w2v_ingest* g = nullptr;
+  check(w2v_ingest_create(gpu_device, fmt == w2v_corpus::kText8 ? W2V_INGEST_TEXT8 : W2V_INGEST_LINES,
+                          ingest_chunk_bytes, &g),
+        "w2v_ingest_create");
+  ingest_ = g;
+  check(w2v_ingest_count(g, f.data(), (int64_t)f.size()), "w2v_ingest_count");
+  int64_t n_words = 0;
+  check(w2v_ingest_summary(g, &n_words, nullptr, nullptr), "w2v_ingest_summary");
+  std::vector<int64_t> first((size_t)n_words);
+  std::vector<int32_t> len((size_t)n_words);
+  ingest_counts_.assign((size_t)n_words, 0);
+  check(w2v_ingest_words(g, first.data(), len.data(), ingest_counts_.data()), "w2v_ingest_words");
+  ingest_words_.resize((size_t)n_words);
+  for (size_t k = 0; k < (size_t)n_words; ++k) ingest_words_[k].assign(f.data() + first[k], (size_t)len[k]);
+  ingest_key_ = key;
+}
+
 void Word2Vec::file_samples(const std::string& path, const std::string& format, int threads,
                             std::vector<int32_t>& ids, std::vector<int64_t>& offsets, int64_t& train_words) {
+  if (gpu_ingest) {
+    ingest_count(path, format);
+    std::vector<int32_t> index(ingest_words_.size(), -1);
+    for (size_t k = 0; k < ingest_words_.size(); ++k) {
+      auto it = vocab_hash.find(ingest_words_[k]);
+      if (it != vocab_hash.end()) index[k] = (int32_t)it->second->index;
+    }
+    const w2v_corpus::File f(path);
+    check(w2v_ingest_map(ingest_, f.data(), (int64_t)f.size(), index.data(), (int64_t)index.size()), "w2v_ingest_map");
+    int64_t n_ids = 0, n_sent = 0;
+    check(w2v_ingest_samples_size(ingest_, &n_ids, &n_sent, &train_words), "w2v_ingest_samples_size");
+    ids.resize((size_t)n_ids);
+    offsets.resize((size_t)n_sent + 1);
+    check(w2v_ingest_download(ingest_, ids.data(), offsets.data()), "w2v_ingest_download");
+    return;
+  }
   std::unordered_map<std::string, int32_t> index;
   index.reserve(vocab.size());
   for (const Word* w : vocab) index[w->text] = (int32_t)w->index;

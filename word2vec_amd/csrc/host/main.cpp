@@ -7,7 +7,7 @@
 // the pre-override 0.025 (:116), 1000-token sentences (:66), and which matrix
 // is written (:196-201). Additive: -train is honoured (the reference always
 // reads ./text8), -binary, -gpu, -replay, -shared-negatives, and the
-// multi-GPU flags -gpus, -sync-words, -overlap (Word2Vec::gpu_devices).
+// multi-GPU flags -gpus, -sync-words, -overlap (Word2Vec::gpu_devices), -gpu-ingest.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -42,7 +42,8 @@ void usage() {
                "  -shared-negatives <0|1> skip-gram NS as the shared-negatives minibatch on the matrix cores\n"
                "  -gpus <int>           data-parallel replicas on devices gpu .. gpu+n-1, averaged with RCCL (default 1)\n"
                "  -sync-words <int>     average the replicas every this many words of a shard (default 0: per epoch)\n"
-               "  -overlap <0|1>        overlap the averaging with the next round's training (default 1)\n\n"
+               "  -overlap <0|1>        overlap the averaging with the next round's training (default 1)\n"
+               "  -gpu-ingest <0|1>     count and map the corpus on the GPU (default 0: host threads)\n\n"
                "example: ./word2vec -train text8 -output vec.txt -size 300 -window 5 -subsample 1e-4 "
                "-negative 5 -model sg -train_method ns -iter 3\n";
 }
@@ -72,7 +73,7 @@ int main(int argc, char** argv) {
   float init_alpha = 0.025f, subsample_threshold = 0.0001f;
   const float min_alpha = init_alpha * 0.0001;
   const bool cbow_mean = true;
-  int binary = 0, gpu = 0, replay = 0, shared = 0, gpus = 1, overlap = 1;
+  int binary = 0, gpu = 0, replay = 0, shared = 0, gpus = 1, overlap = 1, gpu_ingest = 0;
   long long sync_words = 0;
   int i;
   if ((i = find_flag("-size", argc, argv)) > 0) word_dim = std::atoi(argv[i + 1]);
@@ -96,6 +97,7 @@ int main(int argc, char** argv) {
   if ((i = find_flag("-gpus", argc, argv)) > 0) gpus = std::atoi(argv[i + 1]);
   if ((i = find_flag("-sync-words", argc, argv)) > 0) sync_words = std::atoll(argv[i + 1]);
   if ((i = find_flag("-overlap", argc, argv)) > 0) overlap = std::atoi(argv[i + 1]);
+  if ((i = find_flag("-gpu-ingest", argc, argv)) > 0) gpu_ingest = std::atoi(argv[i + 1]);
   if (gpus < 1 || sync_words < 0) {
     std::cout << "Please set -gpus >= 1 and -sync-words >= 0!" << std::endl;
     return 1;
@@ -132,6 +134,7 @@ int main(int argc, char** argv) {
     for (int k = 0; k < gpus; ++k) w2v.gpu_devices.push_back(gpu + k);
   w2v.sync_words = sync_words;
   w2v.overlap_average = overlap != 0;
+  w2v.gpu_ingest = gpu_ingest != 0;
   // main.cpp:63-92's reader (1000-token sentences), streamed from the mapped
   // file by host threads: the same vocabulary and samples as building
   // vector<vector<string>> first (Word2Vec::build_vocab_file / train_file)

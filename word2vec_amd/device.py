@@ -131,6 +131,14 @@ class DeviceTrainer:
                   "w2v_dev_upload_corpus")
         self.n_sent = o.size - 1
 
+    def adopt_corpus(self, ingest):
+        """w2v_dev_adopt_corpus: the samples of a mapped GpuIngest (word2vec_amd/ingest.py), device to device."""
+        self._chk(self.lib.w2v_dev_adopt_corpus(self.h, ingest.g), "w2v_dev_adopt_corpus")
+        ni, ns, tw = C.c_int64(), C.c_int64(), C.c_int64()
+        self._chk(self.lib.w2v_ingest_samples_size(ingest.g, C.byref(ni), C.byref(ns), C.byref(tw)),
+                  "w2v_ingest_samples_size")
+        self.n_sent = ns.value
+
     def upload_replay(self, stream, offsets):
         s = np.ascontiguousarray(stream, dtype=np.uint32)
         o = np.ascontiguousarray(offsets, dtype=np.int64)

@@ -33,6 +33,7 @@ def _load():
             "w2v_model_context_policy": (None, [P, I32, I32]),
             "w2v_model_set_shared_negatives": (None, [P, I32]),
             "w2v_model_replicas": (None, [P, P, I32, I64, I32]),
+            "w2v_model_set_gpu_ingest": (None, [P, I32, I64]),
             "w2v_model_build_vocab": (C.c_int, [P, S, I64]),
             "w2v_model_train": (C.c_int, [P, S, I64]),
             "w2v_model_train_ids": (C.c_int, [P, P, P, I64, I64]),
@@ -87,7 +88,8 @@ class Word2Vec:
                  subsample_threshold=0.001, init_alpha=0.025, min_alpha=1e-6, cbow_mean=False, num_threads=1,
                  train_method="hs", model="cbow", gpu_device=0, replay_rng=False, verbose=False, hot_rows=-2,
                  private_rows=-1, flush_centers=0, private_average=8.0, max_waves=0, shared_negatives=False,
-                 context_rows=-1, context_flush=0, gpu_devices=None, sync_words=0, overlap_average=True):
+                 context_rows=-1, context_flush=0, gpu_devices=None, sync_words=0, overlap_average=True,
+                 gpu_ingest=False, ingest_chunk_bytes=0):
         self.L = _load()
         self.word_dim = word_dim
         self.h = self.L.w2v_model_new(iter, window, min_count, table_size, word_dim, negative, subsample_threshold,
@@ -103,6 +105,7 @@ class Word2Vec:
         if gpu_devices:
             devs = np.ascontiguousarray(gpu_devices, np.int32)
             self.L.w2v_model_replicas(self.h, _p(devs), devs.size, int(sync_words), int(bool(overlap_average)))
+        self.L.w2v_model_set_gpu_ingest(self.h, int(bool(gpu_ingest)), int(ingest_chunk_bytes))
 
     def __del__(self):
         try:
@@ -204,7 +207,7 @@ class Word2Vec:
 
     def vocab(self):
         V = self.V
-        words = [self.L.w2v_model_word(self.h, i).decode() for i in range(V)]  # indices in range: never NULL
+        words = [self.L.w2v_model_word(self.h, i).decode("utf-8", errors="surrogateescape") for i in range(V)]  # indices in range: never NULL
         counts = np.array([self.L.w2v_model_word_count(self.h, i) for i in range(V)], np.int64)
         return words, counts
 
