@@ -16,6 +16,7 @@ PASS[sq2]="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INST
 PASS[tcc]="TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_avr"
 PASS[fetch]="FETCH_SIZE"
 PASS[write]="WRITE_SIZE"
+PASS[atom]="TCC_EA0_ATOMIC_sum TCC_EA0_WRREQ_sum TCC_EA0_RDREQ_sum"
 for p in ${PASSES:-sq1 sq2 tcc fetch write}; do
   timeout -s KILL 120 rocprofv3 --pmc ${PASS[$p]} --output-format csv -d "$OUT/$p" -o $p -- python3 "${BENCH[@]}" > "$OUT/$p.json" 2> "$OUT/$p.err"
   echo "pass $p done"

@@ -53,8 +53,13 @@ template <int NV>
 constexpr int kMaxBlock = NV <= 6 ? 1024 : 256;
 // Waves per SIMD the epoch kernel is compiled for: two 16-wave workgroups per
 // CU when a row is <= 2 floats per lane (d <= 128: 64 VGPRs), else one.
+#ifndef W2V_MIN_WAVES
 template <int NV>
 constexpr int kMinWaves = NV <= 2 ? 8 : 4;
+#else  // occupancy experiments (tools/r02/occ_probe.sh)
+template <int NV>
+constexpr int kMinWaves = W2V_MIN_WAVES;
+#endif
 
 struct TrainArgs {
   float* W;
@@ -114,6 +119,18 @@ constexpr int kSnPrivBytes = 16 * 1024;
 
 struct Counters {
   unsigned long long centers = 0, contexts = 0, targets = 0, draws = 0, sentences = 0;
+  // Phase timing (diagnostic builds only: make prof, -DW2V_PP_PROF=1;
+  // tools/pp_prof.sh): s_memtime since the previous stamp, summed per phase.
+#ifdef W2V_PP_PROF
+  unsigned long long t = 0, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  __device__ void stamp(int k) {
+    const unsigned long long now = __builtin_amdgcn_s_memtime();
+    acc[k] += now - t;
+    t = now;
+  }
+#else
+  __device__ void stamp(int) {}
+#endif
 };
 
 // stats[kNonFinite] counts sigma arguments (row . input dot products) that
@@ -421,10 +438,100 @@ __device__ __forceinline__ void flush_private(const TrainArgs& a, const PrivRows
   }
 }
 
-// HS on the path of `word` (synapses1 rows).
+// HS on the path of `word` (synapses1 rows), software-pipelined: the path's
+// nodes are known up front and distinct, so batch b + 1's rows are gathered
+// BEFORE batch b's updates are issued. vmcnt retires in order on gfx950, so a
+// gather issued after a batch's stores and memory-side atomics would wait for
+// all of them (~3000 cycles per atomic with every CU issuing); issued before
+// them it waits only for its own loads. Same arithmetic, same order of the
+// gradient sum as apply_targets (target order), so the sequential schedule
+// stays bit-exact.
+template <int NV, int MT>
+__device__ __forceinline__ void hs_gather(const TrainArgs& a, int T, int row_l, int t0, const PrivRows& pr, int lane,
+                                          float (&r)[MT][NV]) {
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    if (t < T) {
+      const int row = readlane_i(row_l, t0 + t);
+#ifdef W2V_PP_NOPRIVLOAD  // timing experiment only (wrong numerics): privatised rows skip their global load
+      if (pr.has(row)) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) r[t][v] = 0.f;
+        continue;
+      }
+#endif
+      load_row<NV>(a.S, row, a.pitch, a.dim, lane, pr.has(row) || row >= a.hot_s, r[t]);
+    }
+  }
+}
+
+// Scores of a gathered batch: privatised rows get the pending delta, then
+// g += gt * row (pre-update row, :244) in target order; returns gt per target.
+template <int NV, int MT>
+__device__ __forceinline__ void hs_score(const TrainArgs& a, int T, int row_l, int code_l, int t0, const PrivRows& pr,
+                                         int lane, const float (&x)[NV], float (&g)[NV], float alpha,
+                                         float (&r)[MT][NV], float (&gt)[MT]) {
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+    if (t < T) {
+      const int row = readlane_i(row_l, t0 + t);
+      if (pr.has(row)) priv_read<NV>(pr, row, lane, r[t]);
+    }
+  float f[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    f[t] = 0.f;
+    if (t < T) {
+      float p = 0.f;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) p += r[t][v] * x[v];
+      f[t] = wave_sum(p);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    gt[t] = 0.f;
+    if (t < T) {
+      const int code = readlane_i(code_l, t0 + t);
+      note_nonfinite(a.stats, !__builtin_isfinite(f[t]), lane);
+      const float e = expf(-f[t]);
+      const float s = (float)(1.0 / (1.0 + (double)e));
+      gt[t] = (float)((1.0 - (double)code - (double)s) * (double)alpha);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) g[v] += gt[t] * r[t][v];
+    }
+  }
+}
+
+// The updates of a scored batch: LDS delta (privatised), memory-side atomic
+// (hot), or the updated row stored (Hogwild).
+template <int NV, int MT>
+__device__ __forceinline__ void hs_apply(const TrainArgs& a, int T, int row_l, int t0, const PrivRows& pr, int lane,
+                                         const float (&x)[NV], float (&r)[MT][NV], const float (&gt)[MT]) {
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    if (t < T) {
+      const int row = readlane_i(row_l, t0 + t);
+      float delta[NV];
+#pragma unroll
+      for (int v = 0; v < NV; ++v) delta[v] = gt[t] * x[v];
+      if (pr.has(row)) {
+        priv_add<NV>(pr, row, a.dim, lane, delta);
+      } else if (row >= a.hot_s) {
+        atomic_add_row<NV>(a.S, row, a.pitch, a.dim, lane, delta);
+      } else {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) r[t][v] += delta[v];
+        store_row<NV>(a.S, row, a.pitch, a.dim, lane, r[t]);
+      }
+    }
+  }
+}
+
 template <int NV, int MAXT>
 __device__ __forceinline__ void hs_word(const TrainArgs& a, int word, int lane, const float (&x)[NV],
                                         float (&g)[NV], float alpha, Counters& cnt, float* lds) {
+  constexpr int MT = MAXT / 2 > 0 ? MAXT / 2 : 1;  // two buffers of MT rows: the same registers as one of MAXT
   const PrivRows pr = (a.priv_M == a.S) ? out_rows<NV>(a, lds) : PrivRows();
   const int64_t cb = a.coff[word];
   const int L = (int)(a.coff[word + 1] - cb);
@@ -432,10 +539,20 @@ __device__ __forceinline__ void hs_word(const TrainArgs& a, int word, int lane, 
     const int rem = min(kWave, L - c0);
     const int pt_l = (lane < rem) ? a.points[cb + c0 + lane] : 0;
     const int cd_l = (lane < rem) ? (int)a.codes[cb + c0 + lane] : 0;
-    for (int t0 = 0; t0 < rem; t0 += MAXT) {
-      if (a.strict) drain_vmem();
-      apply_targets<NV, MAXT, true>(a.S, a.pitch, a.dim, lane, min(MAXT, rem - t0), pt_l, cd_l, t0, x, g,
-                                    alpha, a.hot_s, INT64_MAX, pr, a.stats);
+    float ra[MT][NV], rb[MT][NV], gt[MT];
+    if (a.strict) drain_vmem();
+    hs_gather<NV, MT>(a, min(MT, rem), pt_l, 0, pr, lane, ra);
+    for (int t0 = 0; t0 < rem; t0 += 2 * MT) {
+      const int Ta = min(MT, rem - t0), Tb = min(MT, rem - t0 - MT);  // Tb <= 0: no second batch
+      hs_score<NV, MT>(a, Ta, pt_l, cd_l, t0, pr, lane, x, g, alpha, ra, gt);
+      if (Tb > 0) hs_gather<NV, MT>(a, Tb, pt_l, t0 + MT, pr, lane, rb);
+      hs_apply<NV, MT>(a, Ta, pt_l, t0, pr, lane, x, ra, gt);
+      if (Tb > 0) {
+        hs_score<NV, MT>(a, Tb, pt_l, cd_l, t0 + MT, pr, lane, x, g, alpha, rb, gt);
+        const int Tn = min(MT, rem - t0 - 2 * MT);
+        if (Tn > 0) hs_gather<NV, MT>(a, Tn, pt_l, t0 + 2 * MT, pr, lane, ra);
+        hs_apply<NV, MT>(a, Tb, pt_l, t0 + MT, pr, lane, x, rb, gt);
+      }
     }
     cnt.targets += (unsigned long long)rem;
   }
@@ -546,7 +663,9 @@ __device__ __forceinline__ void sg_center(const TrainArgs& a, float* lds, const 
     }
     ++slot;
   }
+  cnt.stamp(3);
   add_to_row<NV>(a.W, c, hot_c, a.pitch, a.dim, lane, g);  // W.row(center) += neu1_grad (:351)
+  cnt.stamp(4);
 }
 
 // ---------------------------------------------------------------------------
@@ -585,6 +704,7 @@ __device__ __forceinline__ void cbow_tail(const TrainArgs& a, float* lds, int i,
 #pragma unroll
     for (int v = 0; v < NV; ++v) h[v] /= nf;
   }
+  cnt.stamp(2);
   if (HS) hs_word<NV, MAXT>(a, c, lane, h, g, alpha, cnt, lds);
   if (NS) {
     const int nd = a.negative;
@@ -592,17 +712,39 @@ __device__ __forceinline__ void cbow_tail(const TrainArgs& a, float* lds, int i,
     cnt.draws += (unsigned long long)nd;
     ns_word<NV, MAXT>(a, a.W, c, negw_l, 0, lane, h, g, alpha, cnt, lds);
   }
+  cnt.stamp(3);
   if (a.cbow_mean) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) g[v] /= nf;
   }
-  for (int r = 0; r < U; ++r) {  // C.row(id) += neu1_grad for every unique id (:315)
-    const int row = row_of(r);
-    if (cx.has(row))
-      priv_add<NV>(cx, row, a.dim, lane, g);
-    else
-      add_to_row<NV>(a.C, row, row < a.hot_wc, a.pitch, a.dim, lane, g);
+  // C.row(id) += neu1_grad for every unique id (:315). The plain (Hogwild)
+  // rows of a batch are all gathered before any of them is stored: with
+  // in-order vmcnt a row-by-row read-modify-write would make each gather wait
+  // for the previous row's store.
+  for (int r0 = 0; r0 < U; r0 += MAXT) {
+    float cur[MAXT][NV];
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t)
+      if (r0 + t < U) {
+        const int row = row_of(r0 + t);
+        if (!cx.has(row) && row >= a.hot_wc) load_row<NV>(a.C, row, a.pitch, a.dim, lane, false, cur[t]);
+      }
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t)
+      if (r0 + t < U) {
+        const int row = row_of(r0 + t);
+        if (cx.has(row)) {
+          priv_add<NV>(cx, row, a.dim, lane, g);
+        } else if (row < a.hot_wc) {
+          atomic_add_row<NV>(a.C, row, a.pitch, a.dim, lane, g);
+        } else {
+#pragma unroll
+          for (int v = 0; v < NV; ++v) cur[t][v] += g[v];
+          store_row<NV>(a.C, row, a.pitch, a.dim, lane, cur[t]);
+        }
+      }
   }
+  cnt.stamp(4);
 }
 
 template <int NV, int MAXT, bool HS, bool NS, bool REPLAY>
@@ -642,6 +784,7 @@ __device__ __forceinline__ void cbow_center(const TrainArgs& a, float* lds, cons
       if (lane == rk) sid = v;
     }
   }
+  cnt.stamp(1);
   cbow_tail<NV, MAXT, HS, NS, REPLAY>(a, lds, i, c, n, U, [&](int r) { return readlane_i(sid, r); }, s, alpha, rp,
                                       cnt, lane);
 }
@@ -727,6 +870,7 @@ template <int NV, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY, bool WIDE>
 __device__ __forceinline__ void center(const TrainArgs& a, float* lds, const int32_t* sent, int len, int i, int c,
                                        int rw, uint32_t s, float alpha, const uint32_t*& rp, Counters& cnt,
                                        int lane) {
+  cnt.stamp(0);
   if (CBOW && WIDE)
     cbow_center_wide<NV, MAXT, HS, NS, REPLAY, kWideChunks>(a, lds, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
   else if (CBOW)
@@ -742,8 +886,11 @@ __device__ __forceinline__ void center(const TrainArgs& a, float* lds, const int
     unsigned n = 0;
     if (lane == 0) n = atomicAdd(done, 1u) + 1u;
     n = (unsigned)__builtin_amdgcn_readfirstlane((int)n);
+    cnt.stamp(7);
     if (a.priv_n > 0 && n % (unsigned)a.flush_every == 0u) flush_private<NV>(a, out_rows<NV>(a, lds), lane);
+    cnt.stamp(5);
     if (a.ctx_n > 0 && n % (unsigned)a.ctx_flush_every == 0u) flush_private<NV>(a, ctx_rows<NV>(a, lds), lane);
+    cnt.stamp(6);
   }
 }
 
@@ -761,6 +908,9 @@ __global__ __launch_bounds__(kMaxBlock<NV>, kMinWaves<NV>) void train_epoch_kern
     __syncthreads();
   }
   Counters cnt;
+#ifdef W2V_PP_PROF
+  cnt.t = __builtin_amdgcn_s_memtime();
+#endif
   float alpha = a.init_alpha;
   bool first = true;
   const uint32_t wmax = (uint32_t)(a.window < 1 ? 1 : a.window);
@@ -836,6 +986,13 @@ __global__ __launch_bounds__(kMaxBlock<NV>, kMinWaves<NV>) void train_epoch_kern
   }
   flush_private<NV>(a, out_rows<NV>(a, lds), lane);
   flush_private<NV>(a, ctx_rows<NV>(a, lds), lane);
+#ifdef W2V_PP_PROF
+  cnt.stamp(0);
+  if (lane == 0 && (threadIdx.x / kWave) % 4 == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))
+    printf("PPPROF block %u wave %d centers %llu: %llu %llu %llu %llu %llu %llu %llu %llu\n", blockIdx.x,
+           (int)(threadIdx.x / kWave), cnt.centers, cnt.acc[0], cnt.acc[1], cnt.acc[2], cnt.acc[3], cnt.acc[4],
+           cnt.acc[5], cnt.acc[6], cnt.acc[7]);
+#endif
   if (lane == 0) {
     atomicAdd(&a.stats[0], cnt.centers);
     atomicAdd(&a.stats[1], cnt.contexts);
