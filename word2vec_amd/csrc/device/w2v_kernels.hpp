@@ -115,7 +115,11 @@ struct TrainArgs {
 };
 
 // LDS the shared-negatives kernel gives its private C rows (w2v_shared.hpp kSnPriv; <= 32 rows).
+#ifndef W2V_SN_PRIV_BYTES
 constexpr int kSnPrivBytes = 16 * 1024;
+#else  // experiments (tools/r02/sn_slots_probe.sh)
+constexpr int kSnPrivBytes = W2V_SN_PRIV_BYTES;
+#endif
 
 struct Counters {
   unsigned long long centers = 0, contexts = 0, targets = 0, draws = 0, sentences = 0;
