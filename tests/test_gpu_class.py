@@ -115,8 +115,31 @@ def test_cli_end_to_end(tmp_path):
     assert vals.size == 64 and np.isfinite(vals).all()
 
 
+def test_cli_gpu_ingest_identical(tmp_path):
+    """The CLI with -gpu-ingest 1 (vocab count and id mapping on the GPU)
+    writes the same vocab file and the same words in the same order as with the
+    host readers (the CLI seeds its generator from std::random_device, as the
+    reference does, so the vectors themselves differ from run to run)."""
+    sents = zipf_sentences(30, 1000, 2000, seed=18)
+    corpus = tmp_path / "corpus.txt"
+    corpus.write_text(" ".join(" ".join(s) for s in sents))
+    outs = []
+    for gi in ("0", "1"):
+        out, vocab = tmp_path / f"vec{gi}.txt", tmp_path / f"vocab{gi}.txt"
+        r = subprocess.run([str(ROOT / "word2vec_amd" / "bin" / "word2vec"), "-train", str(corpus), "-output", str(out),
+                            "-size", "32", "-negative", "5", "-iter", "1", "-replay", "1", "-save-vocab", str(vocab),
+                            "-gpu-ingest", gi], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+        outs.append((vocab.read_text(), out.read_text()))
+    assert outs[0][0] == outs[1][0]
+    w0 = [l.split()[0] for l in outs[0][1].splitlines()[1:]]
+    w1 = [l.split()[0] for l in outs[1][1].splitlines()[1:]]
+    assert w0 == w1 and outs[0][1].splitlines()[0] == outs[1][1].splitlines()[0]
+
+
+@pytest.mark.parametrize("gpu_ingest", [False, True])
 @pytest.mark.parametrize("mode", ["sg_ns", "cbow_hs"])
-def test_class_train_file_equals_train(tmp_path, mode):
+def test_class_train_file_equals_train(tmp_path, mode, gpu_ingest):
     """train_file (mapped corpus, threaded tokenisation) trains exactly what
     train(line_docs(path)) does: replay mode is deterministic, so the matrices
     must be identical."""
@@ -128,7 +151,7 @@ def test_class_train_file_equals_train(tmp_path, mode):
     m = MODES[mode]
     b = Word2Vec(iter=1, window=5, min_count=2, table_size=50_000, word_dim=32, negative=m["negative"],
                  subsample_threshold=1e-3, init_alpha=0.05, min_alpha=2.5e-6, cbow_mean=True,
-                 train_method=m["train_method"], model=m["model"], replay_rng=True)
+                 train_method=m["train_method"], model=m["model"], replay_rng=True, gpu_ingest=gpu_ingest)
     b.seed(5)
     b.build_vocab_file(path, "lines", 2)
     b.init_weights()
