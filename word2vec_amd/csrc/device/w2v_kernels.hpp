@@ -457,13 +457,6 @@ __device__ __forceinline__ void hs_gather(const TrainArgs& a, int T, int row_l, 
   for (int t = 0; t < MT; ++t) {
     if (t < T) {
       const int row = readlane_i(row_l, t0 + t);
-#ifdef W2V_PP_NOPRIVLOAD  // timing experiment only (wrong numerics): privatised rows skip their global load
-      if (pr.has(row)) {
-#pragma unroll
-        for (int v = 0; v < NV; ++v) r[t][v] = 0.f;
-        continue;
-      }
-#endif
       load_row<NV>(a.S, row, a.pitch, a.dim, lane, pr.has(row) || row >= a.hot_s, r[t]);
     }
   }
