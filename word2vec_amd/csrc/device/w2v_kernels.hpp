@@ -46,6 +46,14 @@
 namespace w2v {
 
 constexpr int kWave = 64;
+// Timing-only experiment builds (tools/r02/exp_variant.sh; never the product):
+// bit 1 skips the hot-row atomics of the targets, bit 2 the global atomics of
+// the private-row flushes, bit 4 the hot context-row atomics of CBOW; in the
+// shared-negatives kernel bit 8 skips the staged atomic rows, bit 16 the
+// private-row flush atomics, bit 32 makes the coherent (sc1) stores plain.
+#ifndef W2V_EXP_SKIP
+#define W2V_EXP_SKIP 0
+#endif
 // Largest workgroup per row width: up to 16 waves share one LDS region of
 // privatised rows while the register budget (<=128 VGPRs at 4 waves/SIMD)
 // holds; wider rows keep 4-wave workgroups.
@@ -389,7 +397,7 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
       if (priv[t]) {  // ds_add_f32 into the workgroup's delta; flushed after the center
         priv_add<NV>(pr, rows[t], d, lane, delta);
       } else if (hot[t]) {
-        atomic_add_row<NV>(M, rows[t], pitch, d, lane, delta);
+        if (!(W2V_EXP_SKIP & 1)) atomic_add_row<NV>(M, rows[t], pitch, d, lane, delta);
       } else {
 #pragma unroll
         for (int v = 0; v < NV; ++v) r[t][v] += delta[v];
@@ -435,7 +443,7 @@ __device__ __forceinline__ void flush_private(const TrainArgs& a, const PrivRows
     for (int v = 0; v < NV; ++v) {
       if (lane + kWave * v < a.dim) {
         const float val = atomicExch(q + kWave * v, 0.0f);
-        if (val != 0.0f)
+        if (val != 0.0f && !(W2V_EXP_SKIP & 2))
           (void)__hip_atomic_fetch_add(dst + kWave * v, val * sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -515,7 +523,7 @@ __device__ __forceinline__ void hs_apply(const TrainArgs& a, int T, int row_l, i
       if (pr.has(row)) {
         priv_add<NV>(pr, row, a.dim, lane, delta);
       } else if (row >= a.hot_s) {
-        atomic_add_row<NV>(a.S, row, a.pitch, a.dim, lane, delta);
+        if (!(W2V_EXP_SKIP & 1)) atomic_add_row<NV>(a.S, row, a.pitch, a.dim, lane, delta);
       } else {
 #pragma unroll
         for (int v = 0; v < NV; ++v) r[t][v] += delta[v];
@@ -733,7 +741,7 @@ __device__ __forceinline__ void cbow_tail(const TrainArgs& a, float* lds, int i,
         if (cx.has(row)) {
           priv_add<NV>(cx, row, a.dim, lane, g);
         } else if (row < a.hot_wc) {
-          atomic_add_row<NV>(a.C, row, a.pitch, a.dim, lane, g);
+          if (!(W2V_EXP_SKIP & 4)) atomic_add_row<NV>(a.C, row, a.pitch, a.dim, lane, g);
         } else {
 #pragma unroll
           for (int v = 0; v < NV; ++v) cur[t][v] += g[v];

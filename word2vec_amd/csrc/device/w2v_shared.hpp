@@ -119,7 +119,7 @@ __device__ __forceinline__ f32x4 load_row4(__amdgpu_buffer_rsrc_t r, uint32_t of
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
 }
 __device__ __forceinline__ void store_row4(f32x4 v, __amdgpu_buffer_rsrc_t r, uint32_t off, bool coherent) {
-  if (coherent) __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kSc1);
+  if (coherent && !(W2V_EXP_SKIP & 32)) __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kSc1);
   else __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
 }
 
@@ -388,7 +388,8 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<KB, NW>& 
 #pragma unroll
       for (int cc = 0; cc < kCols; cc += kWave)
         if (cc + lane < kCols)
-          (void)__hip_atomic_fetch_add(dst + cc + lane, src[cc + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (!(W2V_EXP_SKIP & 8))
+            (void)__hip_atomic_fetch_add(dst + cc + lane, src[cc + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     wave_lds_order();
   }
@@ -418,7 +419,8 @@ __device__ __forceinline__ void sn_flush_private(const TrainArgs& a, SnShared<KB
       float* p = &sh.priv[r][wave * kCols + cc];
       const float v = *p;
       *p = 0.f;
-      if (v != 0.f) (void)__hip_atomic_fetch_add(dst + cc, v * sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v != 0.f && !(W2V_EXP_SKIP & 16))
+        (void)__hip_atomic_fetch_add(dst + cc, v * sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   wave_lds_order();
