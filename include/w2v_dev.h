@@ -218,6 +218,12 @@ int w2v_dev_set_hot_auto(w2v_dev* h, float tau_rows, float tau_nodes);
 /* The update policy the last parallel launch used: hot W / C rows, hot
  * Huffman nodes, LDS-private output rows, LDS-private context rows. */
 int w2v_dev_policy(w2v_dev* h, int64_t* hot_rows, int64_t* hot_nodes, int32_t* private_rows, int32_t* context_rows);
+/* The flush intervals (workgroup centers) of the LDS-private output and
+ * context rows the last parallel launch used (0 = that range was empty).
+ * Auto for HS: the fewest of 64 / 128 / 256 that still gives every workgroup
+ * >= 128 flushes per launch (context rows at half). Additive; no reference
+ * counterpart. */
+int w2v_dev_flush_policy(w2v_dev* h, int32_t* flush_centers, int32_t* context_flush);
 int w2v_dev_set_private_rows(w2v_dev* h, int32_t n);
 /* With private_rows = -1: privatise only the rows (Huffman nodes for HS, and
  * CBOW context rows) a center updates at least `mu` times on average, from

@@ -163,6 +163,7 @@ struct w2v_dev {
   // per internal node the same summed over the words below it
   uint64_t stats_version = ~0ull;
   bool stats_ok = false;
+  double kept_tokens = 0.0;         // expected kept centers of one epoch over the corpus (sum count * min(1, keep))
   std::vector<double> f, fk, node_f, node_fk;
   double hot_tau_rows = 1.0;        // automatic hot rows: expected concurrent updates threshold, W / C rows
   double hot_tau_nodes = 1.0;       //   ... and Huffman nodes
@@ -170,6 +171,7 @@ struct w2v_dev {
   // the policy the last parallel launch used (w2v_dev_policy)
   int64_t last_hot_rows = 0, last_hot_nodes = 0;
   int32_t last_priv = 0, last_ctx = 0;
+  int32_t last_flush = 0, last_ctx_flush = 0;
 };
 
 namespace w2v {
@@ -197,6 +199,7 @@ static void row_stats(w2v_dev* h) {
     h->stats_ok = false;
     return;
   }
+  h->kept_tokens = K;
   for (int64_t w = 0; w < V; ++w) {
     h->f[(size_t)w] = (double)h->tok_count[(size_t)w] / N;
     h->fk[(size_t)w] = (double)h->tok_count[(size_t)w] * std::min(1.0, (double)h->keep_h[(size_t)w]) / K;
@@ -935,6 +938,27 @@ int w2v_dev_train_sentences_async(w2v_dev* h, int32_t epoch, const int64_t* orde
   return launch_train(h, epoch, order_dev, count);
 }
 
+// Flush interval of the HS privatised rows (auto: flush_centers == 0), in
+// centers of a workgroup: the fewest of 64, 128, 256 that still gives every
+// workgroup at least kHsFlushes flushes per launch (expected kept centers of
+// the launch / its workgroups, from the corpus statistics). Staleness is the
+// model change between flushes, i.e. the launch's fraction between them: a
+// long launch (configs[1]: ~36 K centers per workgroup) can flush less often
+// with the same fraction, a short one (a small corpus, a replica's slice)
+// keeps 64. Measured on configs[1]: 64 / 128 / 256 (context rows at half) run
+// 152 / 1xx / 171 M words/s; the planted corpus (~2.4 K centers per
+// workgroup, stays at 64) loses 3-5 similarity points when forced to 256
+// (profiles/r02u_c2_flush_hotnode_grid_and_quality.log, r02z_*).
+constexpr double kHsFlushes = 128.0;
+static int32_t auto_hs_flush(w2v_dev* h, int64_t count, int64_t G) {
+  row_stats(h);
+  if (!h->stats_ok || h->n_sent <= 0 || G <= 0) return 64;
+  const double cpw = h->kept_tokens * ((double)count / (double)h->n_sent) / (double)G;
+  int32_t fe = 64;
+  while (fe < 256 && 2.0 * fe * kHsFlushes <= cpw) fe *= 2;
+  return fe;
+}
+
 static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int64_t count) {
   w2v::Range range_("w2v launch");
   if (!h->vocab_ready || !h->corpus_ready) return fail(W2V_ERR_STATE, "upload vocab and corpus first");
@@ -1112,6 +1136,8 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     h->last_hot_nodes = 0;
     h->last_priv = a.priv_n;
     h->last_ctx = 0;
+    h->last_flush = a.priv_n > 0 ? a.flush_every : 0;
+    h->last_ctx_flush = 0;
     HIP_TRY(hipMemsetAsync(h->work, 0, sizeof(unsigned int), h->stream));
     hipLaunchKernelGGL(sn_fn, dim3((unsigned)g), dim3(threads), 0, h->stream, a);
     HIP_TRY(hipGetLastError());
@@ -1184,6 +1210,13 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   // helps small launches (CBOW-HS in 16 slices per epoch, text8-like: analogy
   // 24.5 vs 12.2) but over-damps a corpus with fewer sentences than the chip
   // holds waves (planted CBOW-HS: similarity -13 vs the oracle; profiles/r02l_*, r02r_*).
+  if (h->sched == W2V_SCHED_PARALLEL && h->cfg.hs && a.priv_n + a.ctx_n > 0) {
+    const int32_t fe = auto_hs_flush(h, count, (int64_t)grid.x);
+    if (h->flush_centers <= 0) a.flush_every = fe;
+    if (h->context_flush <= 0) a.ctx_flush_every = std::max<int32_t>(1, fe / 2);
+  }
+  h->last_flush = a.priv_n > 0 ? a.flush_every : 0;
+  h->last_ctx_flush = a.ctx_n > 0 ? a.ctx_flush_every : 0;
   priv_scales(h, a, h->knobs.scale_resident ? resident_wg : (int64_t)grid.x, false);
   hipLaunchKernelGGL(fn, grid, block, lds_bytes, h->stream, a);
   HIP_TRY(hipGetLastError());
@@ -1330,6 +1363,13 @@ int w2v_dev_policy(w2v_dev* h, int64_t* hot_rows, int64_t* hot_nodes, int32_t* p
   if (hot_nodes) *hot_nodes = h->last_hot_nodes;
   if (private_rows) *private_rows = h->last_priv;
   if (context_rows) *context_rows = h->last_ctx;
+  return W2V_OK;
+}
+
+int w2v_dev_flush_policy(w2v_dev* h, int32_t* flush_centers, int32_t* context_flush) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (flush_centers) *flush_centers = h->last_flush;
+  if (context_flush) *context_flush = h->last_ctx_flush;
   return W2V_OK;
 }
 

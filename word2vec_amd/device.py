@@ -215,7 +215,10 @@ class DeviceTrainer:
         """The update policy the last parallel launch used."""
         r, n, p, c = C.c_int64(), C.c_int64(), C.c_int32(), C.c_int32()
         self._chk(self.lib.w2v_dev_policy(self.h, C.byref(r), C.byref(n), C.byref(p), C.byref(c)), "w2v_dev_policy")
-        return {"hot_rows": r.value, "hot_nodes": n.value, "private_rows": p.value, "context_rows": c.value}
+        f, cf = C.c_int32(), C.c_int32()
+        self._chk(self.lib.w2v_dev_flush_policy(self.h, C.byref(f), C.byref(cf)), "w2v_dev_flush_policy")
+        return {"hot_rows": r.value, "hot_nodes": n.value, "private_rows": p.value, "context_rows": c.value,
+                "flush_centers": f.value, "context_flush": cf.value}
 
     def set_private_rows(self, n: int):
         """Hottest output rows privatised per workgroup in LDS: -1 auto (default), 0 off."""
