@@ -165,6 +165,19 @@ def test_parallel_runs_and_counts(mode, dim):
     exp_kept = p.sum()
     sd = np.sqrt((p * (1 - p)).sum()) + 1
     assert abs(st["centers"] - exp_kept) < 6 * sd + (0 if mode.startswith("sg") else 0.01 * exp_kept)
+    pol = d.policy()
+    if mode == "cbow_hs":
+        # automatic HS flush interval (w2v_dev.hip auto_hs_flush): a 120 K-token
+        # launch gives each workgroup far fewer than 128 x 128 centers -> 64 / 32
+        assert (pol["flush_centers"], pol["context_flush"]) == (64, 32), pol
+        d.set_private_sync(32, 8.0)  # explicit intervals win over the automatic one
+        d.set_context_private(-1, 16)
+        d.set_progress(0)
+        assert d.train_epoch(0, None)["nonfinite"] == 0
+        pol = d.policy()
+        assert (pol["flush_centers"], pol["context_flush"]) == (32, 16), pol
+    else:
+        assert pol["context_flush"] == 0 and pol["flush_centers"] in (0, 1024), pol
 
 
 @pytest.mark.parametrize("mode", ["sg_ns", "cbow_hs", "sg_hs"])
