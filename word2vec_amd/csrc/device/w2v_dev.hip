@@ -1086,16 +1086,20 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     a.ctx_M = nullptr;
     a.ctx_n = 0;
     a.item0 = 0;
-    // LDS row slots (kSnPriv in w2v_shared.hpp: 16 KiB of rows, <= 32), parallel
+    // LDS row slots (kSnPriv in w2v_shared.hpp: 20 KiB of rows, <= 32), parallel
     // schedule only. The first priv_n hold the workgroup's pending deltas of
     // the hottest C rows, added to HBM with atomics every flush_centers centers
-    // (auto: half the slots, <= 4, every 1024 centers); the rest stage the
-    // atomic rows' deltas of each center. Measured on configs[4]: 4 private
-    // rows + staged atomics 72 M words/s vs 61 M with neither, and higher
-    // planted / text8-like scores (profiles/r01_sn_atomic_rows.log).
+    // (auto: up to 10, every 1024 centers); the rest stage the atomic rows'
+    // deltas of each center. Measured on configs[4]: 4 private rows + staged
+    // atomics 72 M words/s vs 61 M with neither, and higher planted /
+    // text8-like scores (profiles/r01_sn_atomic_rows.log); private rows in
+    // every slot run faster still with the same scores: of 8 slots, 8 private
+    // rows +4 % over 4 + 4 staging; of 10 slots (single transpose buffer), 10
+    // private +3.8 % over 4 (profiles/r02z_priv.log, r02z_c5_slots10.log,
+    // r02z_sn_quality_probe*.log).
     {
       const int64_t slots = std::min<int64_t>(32, w2v::kSnPrivBytes / (h->pitch * (int64_t)sizeof(float)));
-      const int64_t want = h->private_rows < 0 ? std::min<int64_t>(4, slots / 2) : h->private_rows;
+      const int64_t want = h->private_rows < 0 ? std::min<int64_t>(10, slots) : h->private_rows;
       a.priv_n = h->sched == W2V_SCHED_PARALLEL ? (int32_t)std::min<int64_t>({slots, h->V, want}) : 0;
     }
     a.flush_every = h->flush_centers > 0 ? h->flush_centers : 1024;

@@ -122,9 +122,10 @@ struct TrainArgs {
   float ctx_sc[64];            // kCtxMax
 };
 
-// LDS the shared-negatives kernel gives its private C rows (w2v_shared.hpp kSnPriv; <= 32 rows).
+// LDS the shared-negatives kernel gives its row slots (w2v_shared.hpp kSnPriv; <= 32 rows):
+// 20 KiB = 10 rows at d = 512 with four 2-wave workgroups per CU (38.9 KiB each).
 #ifndef W2V_SN_PRIV_BYTES
-constexpr int kSnPrivBytes = 16 * 1024;
+constexpr int kSnPrivBytes = 20 * 1024;
 #else  // experiments (tools/r02/sn_slots_probe.sh)
 constexpr int kSnPrivBytes = W2V_SN_PRIV_BYTES;
 #endif

@@ -33,8 +33,7 @@
 //     gather layout (so the update is a register add and the write-back the
 //     same 16-B stores as the gather); their A operands need the rows with
 //     the column index on lane & 15, produced per block by a 16x16 transpose
-//     through double-buffered per-wave LDS (row stride 20 floats:
-//     conflict-free reads).
+//     through per-wave LDS (row stride 20 floats: conflict-free reads).
 //   * windows are word2vec.c's (and pWord2Vec's): subsampled tokens leave the
 //     sentence, so a window spans kept tokens. Each wave compacts the kept
 //     tokens into an LDS ring (ballot + mbcnt) and stages the unigram-table
@@ -58,7 +57,7 @@ constexpr int kSnRing = 256;    // kept-token ring (holds a 64-center batch, its
 // back every a.flush_every centers, instead of a coherent read-modify-write
 // of those few rows by every center (their write-through traffic serialises
 // on a handful of memory channels: measured, 16 coherent rows cost a third of
-// the throughput). P fills 16 KiB of LDS, at most 32 rows.
+// the throughput). The row slots fill kSnPrivBytes of LDS, at most 32 rows.
 template <int KB, int NW>
 constexpr int kSnPriv = (kSnPrivBytes / (NW * KB * 64)) < 32 ? (kSnPrivBytes / (NW * KB * 64)) : 32;
 
@@ -66,7 +65,7 @@ template <int KB, int NW>
 struct SnShared {
   f32x4 part[2][NW][kWave];                      // partial L tiles, by center parity
   f32x4 e[NW][kWave];                            // per-wave E tile (for its transpose)
-  float tr[NW][2][2][kSnTile * kSnStride];       // per-wave transpose blocks [buffer][W, C]
+  float tr[NW][2][kSnTile * kSnStride];          // per-wave transpose block [W, C] (one buffer: see the update loop)
   // written identically by every wave (read only before the per-center
   // barrier, rewritten only after it): the kept tokens of the sentence (ring,
   // by kept index) and the draws of a batch of <= 64 centers
@@ -338,25 +337,29 @@ __device__ __forceinline__ void sn_center(const TrainArgs& a, SnShared<KB, NW>& 
   float* ws = &sh.priv[a.priv_n + (w_stage ? w_slot : 0)][(int)cb];
   float* cs = &sh.priv[a.priv_n + (c_stage ? c_slot : 0)][(int)cb];
   pf_.stamp(5);
-  // dW^T = C^T E^T and dC^T = W^T E per 16-column block, added in place;
-  // block kb + 1 goes into the other transpose buffer while kb is consumed
-  float* tb[2][2] = {{sh.tr[wave][0][0], sh.tr[wave][0][1]}, {sh.tr[wave][1][0], sh.tr[wave][1][1]}};
-  *reinterpret_cast<f32x4*>(tb[0][0] + col * kSnStride + 4 * q) = wr[0];
-  *reinterpret_cast<f32x4*>(tb[0][1] + col * kSnStride + 4 * q) = cr[0];
+  // dW^T = C^T E^T and dC^T = W^T E per 16-column block, added in place.
+  // Block kb + 1 is written into the same transpose buffer right after block
+  // kb's reads are issued: one wave's LDS operations execute in order, so the
+  // reads return block kb (the fence only keeps the compiler from reordering;
+  // no wait). One buffer instead of two frees 5 KiB per workgroup for two
+  // more LDS row slots (kSnPrivBytes).
+  float* const tw0 = sh.tr[wave][0];
+  float* const tc0 = sh.tr[wave][1];
+  *reinterpret_cast<f32x4*>(tw0 + col * kSnStride + 4 * q) = wr[0];
+  *reinterpret_cast<f32x4*>(tc0 + col * kSnStride + 4 * q) = cr[0];
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) {
     wave_lds_order();
-    const float* tw = tb[kb & 1][0];
-    const float* tc = tb[kb & 1][1];
     float wd[4], cd[4];
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
-      wd[s4] = tw[(4 * s4 + q) * kSnStride + col];  // W[4s + q][16 kb + col]
-      cd[s4] = tc[(4 * s4 + q) * kSnStride + col];  // C[4s + q][16 kb + col]
+      wd[s4] = tw0[(4 * s4 + q) * kSnStride + col];  // W[4s + q][16 kb + col]
+      cd[s4] = tc0[(4 * s4 + q) * kSnStride + col];  // C[4s + q][16 kb + col]
     }
+    wave_lds_order();
     if (kb + 1 < KB) {
-      *reinterpret_cast<f32x4*>(tb[(kb + 1) & 1][0] + col * kSnStride + 4 * q) = wr[kb + 1];
-      *reinterpret_cast<f32x4*>(tb[(kb + 1) & 1][1] + col * kSnStride + 4 * q) = cr[kb + 1];
+      *reinterpret_cast<f32x4*>(tw0 + col * kSnStride + 4 * q) = wr[kb + 1];
+      *reinterpret_cast<f32x4*>(tc0 + col * kSnStride + 4 * q) = cr[kb + 1];
     }
     f32x4 dw = zero, dc = zero;
 #pragma unroll
