@@ -74,8 +74,9 @@ def parse():
     ap.add_argument("--hot-rows", type=int, default=-2,
                     help="rows updated with atomics (-2 auto from the corpus statistics, -1 all, 0 none = plain "
                          "Hogwild RMW, k = k most frequent)")
-    ap.add_argument("--hot-auto", type=float, nargs=2, default=[1.0, 1.0], metavar=("ROWS", "NODES"),
-                    help="thresholds of the automatic hot rows (expected updates in flight of a W / C row, a node)")
+    ap.add_argument("--hot-auto", type=float, nargs=2, default=[0.0, 1.0], metavar=("ROWS", "NODES"),
+                    help="thresholds of the automatic hot rows (expected updates in flight of a W / C row, a node; "
+                         "rows 0 = by the vocabulary, the library default)")
     ap.add_argument("--private-rows", type=int, default=-1,
                     help="hottest output rows privatised per workgroup in LDS (-1 auto, 0 off)")
     ap.add_argument("--private-rate", type=float, default=None,
@@ -306,12 +307,22 @@ def main():
         flops = 3 * 2 * 16 * 16 * pitch * delta["centers"] / n_launch
         tf = flops / avg_kernel_s / 1e12
         roofline["kernel"] = "train_shared_neg_kernel"
+        # useful work: the unpadded M x T x d products of each center's three GEMMs; the
+        # kernel counts sum M (contexts) and sum T (targets), and T is ~neg + 1 for
+        # every center, so sum M T ~= sum M x mean T
+        useful = 3 * 2 * d * delta["contexts"] * (delta["targets"] / max(1, delta["centers"])) / n_launch
+        tu = useful / avg_kernel_s / 1e12
         roofline["mfma"] = {"issued_tflops": round(tf, 2), "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                            "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 4), "dtype": "f32 (v_mfma_f32_16x16x4_f32)"}
+                            "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 4), "dtype": "f32 (v_mfma_f32_16x16x4_f32)",
+                            "useful_tflops": round(tu, 2), "useful_frac": round(tu / MFMA_F32_PEAK_TFLOPS, 4),
+                            "useful_note": "6 d sum(M T) over unpadded tiles (M unique contexts, T center + "
+                                           "negatives), sum(M T) ~= sum M x mean T"}
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(args, counts_v, ids_h, soff_h, neg, mode)
+        cpu["gpu_over_cpu"] = round(value / max(cpu["value"], 1e-9), 1)
+        cpu["gpu_over_cpu_per_thread_rng"] = round(value / max(cpu["per_thread_rng_value"], 1e-9), 1)
 
     if rank == 0:
         out = {
@@ -397,18 +408,50 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def host_topology() -> dict:
+    """What the CPU legs may use: the process's affinity set (the threads the
+    legs run), the machine's logical CPUs, sockets / physical cores of the
+    affinity set (sysfs), the cgroup CPU quota and where OMP_NUM_THREADS came
+    from (it is not used to size the legs)."""
+    aff = sorted(os.sched_getaffinity(0))
+    pkgs, cores = set(), set()
+    for c in aff:
+        base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+        try:
+            pkg = open(base + "physical_package_id").read().strip()
+            core = open(base + "core_id").read().strip()
+        except OSError:
+            continue
+        pkgs.add(pkg)
+        cores.add((pkg, core))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"affinity_cpus": len(aff), "host_cpus": os.cpu_count(), "sockets": len(pkgs) or None,
+            "physical_cores": len(cores) or None, "cgroup_cpu_quota": quota,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
 def cpu_baseline(args, counts_v, ids_h, soff_h, neg, mode):
     """The reference's OpenMP training loop (Word2Vec.cpp:375-394; restated in
     oracle/w2v_oracle.cpp with its per-call hash map / set, static schedule,
     shared alpha) compiled with the reference's own flags (main.cpp:2: -Ofast
-    -march=native -funroll-loops -fopenmp, built on this host), timed on the
-    host cores over a bounded prefix of the same shard (same params):
-      value                     all OMP_NUM_THREADS threads, ONE shared mt19937 (the reference's data race)
+    -march=native -funroll-loops -fopenmp, built on this host), timed on ALL
+    the host cores this process may run on (len(os.sched_getaffinity(0)), as
+    SURVEY.md §8(d) asks: OMP_NUM_THREADS = nproc; the environment's
+    OMP_NUM_THREADS is reported, not used) over a bounded prefix of the same
+    shard (same params):
+      value                     all affinity threads, ONE shared mt19937 (the reference's data race)
       per_thread_rng_value      the same, one mt19937 per thread
       single_thread_value       one thread"""
     import oracle
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    topo = host_topology()
+    threads = topo["affinity_cpus"]
     path, flags = oracle.build_fast()
     native = oracle.BaselineLib(path)
 
@@ -422,8 +465,9 @@ def cpu_baseline(args, counts_v, ids_h, soff_h, neg, mode):
         return o
 
     def timed(o, nthreads, budget, shared, seed):
-        # calibrate on a small prefix, then time a prefix sized to the budget
-        n_cal = 32
+        # calibrate on a prefix with a few sentences per thread (a static
+        # schedule), then time a prefix sized to the budget
+        n_cal = int(min(soff_h.size - 1, max(32, 4 * nthreads)))
         o.set_samples(ids_h[: soff_h[n_cal]], soff_h[: n_cal + 1], int(n_cal * args.sent_len))
         o.init_weights()
         t = time.perf_counter()
@@ -444,12 +488,12 @@ def cpu_baseline(args, counts_v, ids_h, soff_h, neg, mode):
     return {"value": round(w / dt, 1), "unit": "words/s", "cores": threads, "kind": "port",
             "per_thread_rng_value": round(wp / dtp, 1),
             "single_thread_value": round(w1 / dt1, 1),
-            "cpu": cpu_model(), "host_cpus": os.cpu_count(), "flags": flags,
+            "cpu": cpu_model(), **topo, "flags": flags,
             "sample": f"{n} sentences ({w} in-vocab tokens) of the same shard, {dt:.1f}s: the reference's OpenMP "
                       f"loop restated (oracle/w2v_oracle.cpp orc_train_omp_shared), built with {flags}, "
-                      f"{threads} threads sharing one mt19937 as the reference does; per_thread_rng_value: "
-                      f"{n_p} sentences, {dtp:.1f}s, one mt19937 per thread; single_thread_value: {n1} sentences, "
-                      f"{dt1:.1f}s"
+                      f"{threads} threads (every CPU of the process's affinity set) sharing one mt19937 as the "
+                      f"reference does; per_thread_rng_value: {n_p} sentences, {dtp:.1f}s, one mt19937 per "
+                      f"thread; single_thread_value: {n1} sentences, {dt1:.1f}s"
                       + ("; the reference's per-pair update: the shared-negatives minibatch has no reference CPU path"
                          if mode.get("shared") else "")}
 

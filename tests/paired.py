@@ -96,7 +96,7 @@ def train_gpu_paired(name, mode, seed, sents, max_waves=0, stats=None, policy=No
     if "hot_rows" in pol:
         d.set_hot_rows(pol["hot_rows"])
     if "hot_tau_rows" in pol or "hot_tau_nodes" in pol:
-        d.set_hot_auto(pol.get("hot_tau_rows", 1.0), pol.get("hot_tau_nodes", 1.0))
+        d.set_hot_auto(pol.get("hot_tau_rows", 0.0), pol.get("hot_tau_nodes", 1.0))
     if "private_rows" in pol:
         d.set_private_rows(pol["private_rows"])
     if "private_rate" in pol:

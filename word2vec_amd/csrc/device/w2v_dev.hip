@@ -165,11 +165,12 @@ struct w2v_dev {
   bool stats_ok = false;
   double kept_tokens = 0.0;         // expected kept centers of one epoch over the corpus (sum count * min(1, keep))
   std::vector<double> f, fk, node_f, node_fk;
-  double hot_tau_rows = 1.0;        // automatic hot rows: expected concurrent updates threshold, W / C rows
+  double hot_tau_rows = 0.0;        // automatic hot rows: expected concurrent updates threshold, W / C rows (0 = by vocab, hot_tau_for)
   double hot_tau_nodes = 1.0;       //   ... and Huffman nodes
   double private_rate = 0.0;        // > 0: privatise only rows updated >= this many times per center (private_by_rate)
   // the policy the last parallel launch used (w2v_dev_policy)
   int64_t last_hot_rows = 0, last_hot_nodes = 0;
+  double last_tau_rows = 0.0;
   int32_t last_priv = 0, last_ctx = 0;
   int32_t last_flush = 0, last_ctx_flush = 0;
 };
@@ -867,11 +868,32 @@ static std::pair<int64_t, int64_t> private_by_rate(w2v_dev* h, double mu) {
 // threshold 4 for the W / C rows the planted SG-HS run collapses (analogy
 // 6 vs 89: its center rows, V = 3.4K under 8K waves, fell to plain
 // read-modify-write; profiles/r02c_*). Returns {W / C rows, nodes}.
+// The W / C threshold when hot_tau_rows is 0 (the default): by the average
+// number of a row's updates in flight, rho = waves x (window + 1) / V. A large
+// vocabulary (rho <= 1: configs[2] 0.033, configs[0] 0.2, the text8-like
+// gate corpus 0.5) takes 4: the rows between 1 and 4 expected updates in
+// flight (about a tenth of the update mass under Zipf) race rarely enough for
+// plain read-modify-write, and 1738 -> 435 atomic rows run configs[2] 11 %
+// faster with the text8-like paired scores unchanged
+// (profiles/r02z_hot_tau_probe.log). A small one (the planted corpus, V =
+// 3.4K: rho 14; text8_small, V = 20K: 2.4) keeps 1: at 4 the planted SG-HS
+// center rows fell to plain read-modify-write and the run collapsed
+// (analogy 6 vs 89, profiles/r02c_*). The shared-negatives kernel keeps 1
+// (its floor of 1000 atomic rows decides there).
+constexpr double kHotTauLargeV = 4.0, kHotTauSmallV = 1.0, kHotRhoLargeV = 1.0;
+static double hot_tau_for(const w2v_dev* h, double waves, bool shared) {
+  if (h->hot_tau_rows > 0.0) return h->hot_tau_rows;
+  if (shared || h->V <= 0) return kHotTauSmallV;
+  const double rho = waves * ((double)h->cfg.window + 1.0) / (double)h->V;
+  return rho <= kHotRhoLargeV ? kHotTauLargeV : kHotTauSmallV;
+}
+
 static std::pair<int64_t, int64_t> auto_hot(w2v_dev* h, double waves, bool shared) {
   row_stats(h);
   const int64_t V = h->V;
   if (!h->stats_ok) return {std::min<int64_t>(V, 1000), std::min<int64_t>(std::max<int64_t>(V - 1, 0), 1000)};
-  const double win1 = (double)h->cfg.window + 1.0, tau = h->hot_tau_rows;
+  const double win1 = (double)h->cfg.window + 1.0, tau = hot_tau_for(h, waves, shared);
+  h->last_tau_rows = tau;
   const bool cbow = h->cfg.cbow != 0, ns = h->cfg.negative > 0;
   int64_t rows = 0;
   for (int64_t r = 0; r < V; ++r) {  // largest rate over the row's roles in W and C
@@ -1355,7 +1377,8 @@ int w2v_dev_set_private_rate(w2v_dev* h, float mu) {
 
 int w2v_dev_set_hot_auto(w2v_dev* h, float tau_rows, float tau_nodes) {
   if (!h) return fail(W2V_ERR_ARG, "null handle");
-  if (!(tau_rows > 0.0f) || !(tau_nodes > 0.0f)) return fail(W2V_ERR_ARG, "the automatic hot-row thresholds must be > 0");
+  if (!(tau_rows >= 0.0f) || !(tau_nodes > 0.0f))
+    return fail(W2V_ERR_ARG, "the automatic hot-row thresholds must be >= 0 (rows; 0 = by vocab) and > 0 (nodes)");
   h->hot_tau_rows = tau_rows;
   h->hot_tau_nodes = tau_nodes;
   return W2V_OK;
@@ -1367,6 +1390,13 @@ int w2v_dev_policy(w2v_dev* h, int64_t* hot_rows, int64_t* hot_nodes, int32_t* p
   if (hot_nodes) *hot_nodes = h->last_hot_nodes;
   if (private_rows) *private_rows = h->last_priv;
   if (context_rows) *context_rows = h->last_ctx;
+  return W2V_OK;
+}
+
+int w2v_dev_hot_tau(w2v_dev* h, float* tau_rows, float* tau_nodes) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (tau_rows) *tau_rows = (float)h->last_tau_rows;
+  if (tau_nodes) *tau_nodes = (float)h->hot_tau_nodes;
   return W2V_OK;
 }
 

@@ -207,8 +207,9 @@ class DeviceTrainer:
         0 = none (plain Hogwild RMW), k = the k most frequent."""
         self._chk(self.lib.w2v_dev_set_hot_rows(self.h, int(hot_rows)), "w2v_dev_set_hot_rows")
 
-    def set_hot_auto(self, tau_rows: float = 1.0, tau_nodes: float = 1.0):
-        """Thresholds of the automatic hot rows (expected updates in flight of a W / C row, of a Huffman node)."""
+    def set_hot_auto(self, tau_rows: float = 0.0, tau_nodes: float = 1.0):
+        """Thresholds of the automatic hot rows (expected updates in flight of a W / C row, of a Huffman node);
+        tau_rows 0 = by the vocabulary (the library default: 4 for large V, 1 for small)."""
         self._chk(self.lib.w2v_dev_set_hot_auto(self.h, float(tau_rows), float(tau_nodes)), "w2v_dev_set_hot_auto")
 
     def policy(self) -> dict:
@@ -217,8 +218,10 @@ class DeviceTrainer:
         self._chk(self.lib.w2v_dev_policy(self.h, C.byref(r), C.byref(n), C.byref(p), C.byref(c)), "w2v_dev_policy")
         f, cf = C.c_int32(), C.c_int32()
         self._chk(self.lib.w2v_dev_flush_policy(self.h, C.byref(f), C.byref(cf)), "w2v_dev_flush_policy")
+        tr, tn = C.c_float(), C.c_float()
+        self._chk(self.lib.w2v_dev_hot_tau(self.h, C.byref(tr), C.byref(tn)), "w2v_dev_hot_tau")
         return {"hot_rows": r.value, "hot_nodes": n.value, "private_rows": p.value, "context_rows": c.value,
-                "flush_centers": f.value, "context_flush": cf.value}
+                "flush_centers": f.value, "context_flush": cf.value, "hot_tau_rows": tr.value}
 
     def set_private_rows(self, n: int):
         """Hottest output rows privatised per workgroup in LDS: -1 auto (default), 0 off."""
