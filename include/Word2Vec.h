@@ -144,13 +144,24 @@ class Word2Vec {
   // build_sample of a corpus file as token ids (what train_file trains on).
   void file_samples(const std::string& path, const std::string& format, int threads, std::vector<int32_t>& ids,
                     std::vector<int64_t>& offsets, int64_t& train_words);
-  // Checkpoints between train() calls: W, C, synapses1, the
-  // word counter and the generator state. After load_checkpoint the next
-  // train() / train_ids() / train_file() continues from the restored weights
-  // (no init_weights) with current_words starting at the saved count.
+  // Checkpoints: W, C, synapses1, the word counter, the epochs
+  // of the `iter` schedule done, the device RNG key and the generator state.
+  // With checkpoint_path set, train() / train_ids() / train_file() write one
+  // after every epoch ("%d" in the path = the epochs done, else overwritten).
+  // After load_checkpoint the next train call starts from the restored
+  // weights (no init_weights): a checkpoint taken mid-schedule (epochs done <
+  // iter) runs the remaining epochs with the saved counter, key and shuffle
+  // stream, i.e. continues that run (alpha follows the original schedule);
+  // one taken after the whole schedule starts a new schedule on the loaded
+  // weights (current_words from 0, as every train() of the reference,
+  // Word2Vec.cpp:359). load_checkpoint checks every matrix's shape against
+  // this object's vocab, word_dim, model and train_method and changes nothing
+  // unless all of it is valid.
+  std::string checkpoint_path;
   void save_checkpoint(const std::string& path);
   void load_checkpoint(const std::string& path);
   int64_t current_words() const { return cur_words_; }
+  int64_t epochs_done() const { return epochs_done_; }
   // Last device error (empty if none).
   std::string last_error;
 
@@ -161,6 +172,12 @@ class Word2Vec {
   int64_t cur_words_ = 0;           // current_words after the last train call
   bool resume_ = false;             // load_checkpoint: the next train continues (no init_weights)
   int64_t start_words_ = 0;         //   ... from this current_words
+  int64_t resume_epochs_ = 0;       //   ... after this many epochs of the schedule
+  uint64_t resume_key_ = 0;         //   ... with this Philox key
+  int64_t epochs_done_ = 0;         // epochs of the last train call's schedule completed
+  uint64_t key_ = 0;                // Philox key of the last train call
+  void write_checkpoint(const std::string& path, int64_t cw, int64_t epochs_done, uint64_t key);
+  void checkpoint_epoch(int64_t cw, int64_t epochs_done, uint64_t key);
   w2v_ingest* ingest_ = nullptr;    // gpu_ingest: the counted file ...
   std::string ingest_key_;          //   ... (path + format)
   std::vector<std::string> ingest_words_;  // its distinct words, in order of first occurrence

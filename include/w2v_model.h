@@ -85,6 +85,10 @@ int w2v_model_save_vocab(w2v_model* m, const char* path);
  * generator state; the next train continues from them) and current_words(). */
 int w2v_model_save_checkpoint(w2v_model* m, const char* path);
 int w2v_model_load_checkpoint(w2v_model* m, const char* path);
+/* Word2Vec::checkpoint_path: a checkpoint after every epoch of train ("" = off;
+ * "%d" = the epochs done); epochs of the last train call's schedule done. */
+int w2v_model_set_checkpoint_path(w2v_model* m, const char* path);
+int64_t w2v_model_epochs_done(w2v_model* m);
 int64_t w2v_model_current_words(w2v_model* m);
 int w2v_model_read_vocab(w2v_model* m, const char* path);
 

@@ -189,3 +189,29 @@ def test_checkpoint_round_trip(tmp_path):
     c.build_vocab(sents[:10])
     with pytest.raises(RuntimeError, match="vocabulary"):
         c.load_checkpoint(tmp_path / "ck.bin")
+
+
+def test_checkpoint_load_rejects_bad_shapes(tmp_path):
+    """load_checkpoint checks every matrix against the object's shapes and
+    changes nothing when one is wrong (an NS checkpoint into an HS object)."""
+    import pytest as _pytest
+
+    from tests.corpus import zipf_sentences
+    from word2vec_amd.model import Word2Vec
+
+    sents = zipf_sentences(20, 100, 200, seed=5)
+    ns = Word2Vec(iter=1, window=5, min_count=2, table_size=10_000, word_dim=16, negative=5, train_method="ns",
+                  model="sg")
+    ns.seed(1)
+    ns.build_vocab(sents)
+    ns.init_weights()
+    ns.save_checkpoint(tmp_path / "ns.bin")
+    hs = Word2Vec(iter=1, window=5, min_count=2, table_size=10_000, word_dim=16, negative=5, train_method="hs",
+                  model="sg")
+    hs.seed(1)
+    hs.build_vocab(sents)
+    hs.init_weights()
+    before = hs.matrix(0)
+    with _pytest.raises(RuntimeError, match="checkpoint"):
+        hs.load_checkpoint(tmp_path / "ns.bin")
+    np.testing.assert_array_equal(hs.matrix(0), before)

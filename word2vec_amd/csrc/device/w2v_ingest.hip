@@ -472,7 +472,13 @@ int grow(w2v_ingest* g, int64_t need) {
   return W2V_OK;
 }
 
+// hipcub's element counts are int: a chunk is at most INT32_MAX - 64 bytes
+// (chunk_size_limit; the callers cut the file into such chunks), so its tokens
+// (<= bytes / 2 + 1), tiles (<= bytes / 4096 + 2), the table (<= 2^30 slots,
+// kMaxCap) and the words (<= 2^29) all fit the (int) casts below.
 int ensure_work(w2v_ingest* g, int64_t bytes) {
+  if (bytes < 0 || bytes > (int64_t)INT32_MAX - 64)
+    return fail_i(W2V_ERR_UNSUPPORTED, "w2v_ingest: a chunk must be < 2^31 - 64 bytes (hipcub int counts)");
   if (g->work_cap >= bytes) return W2V_OK;
   dfree(g->buf); dfree(g->tile); dfree(g->starts); dfree(g->nl_after); dfree(g->slot); dfree(g->line_of);
   dfree(g->tok_id); dfree(g->kept); dfree(g->kpos); dfree(g->n_sel);
@@ -656,7 +662,11 @@ int w2v_ingest_count(w2v_ingest* g, const char* data, int64_t n) {
   // a file that fits the residency budget crosses PCIe once: pass 2 reads this copy
   dfree(g->file);
   g->file_n = -1;
-  if (n > 0 && n <= g->resident_max) {
+  // ... and only while it leaves at least half of the device's free memory to
+  // the work buffers, the table and whatever trains next on this device
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+  if (n > 0 && n <= g->resident_max && (uint64_t)n <= (uint64_t)free_b / 2) {
     if (hipMalloc(&g->file, n) == hipSuccess) {
       HIP_I(hipMemcpyAsync(g->file, data, n, hipMemcpyHostToDevice, g->stream));
       g->file_n = n;

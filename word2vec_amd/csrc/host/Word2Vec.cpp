@@ -175,6 +175,12 @@ void Word2Vec::file_samples(const std::string& path, const std::string& format, 
     ids.resize((size_t)n_ids);
     offsets.resize((size_t)n_sent + 1);
     check(w2v_ingest_download(ingest_, ids.data(), offsets.data()), "w2v_ingest_download");
+    // the samples are on the host now: free the ingest handle's device memory
+    // (the resident file, the chunk work buffers, the hash table and the ids)
+    // before training uploads the corpus and the model to the same device
+    w2v_ingest_destroy(ingest_);
+    ingest_ = nullptr;
+    ingest_key_.clear();
     return;
   }
   std::unordered_map<std::string, int32_t> index;
@@ -416,16 +422,21 @@ void Word2Vec::run_epochs(const std::vector<int32_t>& ids, const std::vector<int
   check(w2v_dev_upload_corpus(dev_, ids.data(), (int64_t)ids.size(), offsets.data(), n, train_words),
         "w2v_dev_upload_corpus");
   apply_policy(dev_);
-  check(w2v_dev_set_progress(dev_, resume_ ? start_words_ : 0), "w2v_dev_set_progress");  // current_words = 0 (:359)
+  // a checkpoint taken mid-schedule continues that schedule (its counter, key
+  // and shuffle stream); anything else starts one: current_words = 0 (:359)
+  const bool cont = resume_ && resume_epochs_ > 0 && resume_epochs_ < iter;
+  const int first = cont ? (int)resume_epochs_ : 0;
+  check(w2v_dev_set_progress(dev_, cont ? start_words_ : 0), "w2v_dev_set_progress");
   std::vector<long> sample_idx((size_t)n);
   std::iota(sample_idx.begin(), sample_idx.end(), 0);
-  std::vector<std::vector<int64_t>> orders;
+  std::vector<std::vector<int64_t>> orders((size_t)iter);
+  uint64_t key = 0;
   if (replay_rng) {
     std::vector<uint32_t> stream;
     std::vector<int64_t> stream_off((size_t)(n * iter), 0);
-    for (int it = 0; it < iter; ++it) {
+    for (int it = first; it < iter; ++it) {
       std::shuffle(sample_idx.begin(), sample_idx.end(), generator);
-      orders.emplace_back(sample_idx.begin(), sample_idx.end());
+      orders[(size_t)it].assign(sample_idx.begin(), sample_idx.end());
       append_reference_draws(ids, offsets, sample_idx, stream, stream_off, it);
     }
     check(w2v_dev_upload_replay(dev_, stream.data(), (int64_t)stream.size(), stream_off.data(),
@@ -434,20 +445,31 @@ void Word2Vec::run_epochs(const std::vector<int32_t>& ids, const std::vector<int
     check(w2v_dev_set_rng(dev_, W2V_RNG_REPLAY, 0), "w2v_dev_set_rng");
     check(w2v_dev_set_schedule(dev_, W2V_SCHED_SEQUENTIAL), "w2v_dev_set_schedule");
   } else {
-    const uint64_t key = ((uint64_t)generator() << 32) | (uint64_t)generator();
+    key = cont ? resume_key_ : ((uint64_t)generator() << 32) | (uint64_t)generator();
     check(w2v_dev_set_rng(dev_, W2V_RNG_PHILOX, key), "w2v_dev_set_rng");
     check(w2v_dev_set_schedule(dev_, W2V_SCHED_PARALLEL), "w2v_dev_set_schedule");
   }
-  for (int it = 0; it < iter; ++it) {
+  key_ = key;
+  epochs_done_ = first;
+  resume_ = false;
+  for (int it = first; it < iter; ++it) {
     if (!replay_rng) {
       std::shuffle(sample_idx.begin(), sample_idx.end(), generator);
-      orders.emplace_back(sample_idx.begin(), sample_idx.end());
+      orders[(size_t)it].assign(sample_idx.begin(), sample_idx.end());
     }
     w2v_dev_stats st;
     std::memset(&st, 0, sizeof(st));
     check(w2v_dev_train_epoch(dev_, it, orders[(size_t)it].data(), &st), "w2v_dev_train_epoch");
     int64_t cw = 0;
     check(w2v_dev_get_progress(dev_, &cw), "w2v_dev_get_progress");
+    epochs_done_ = it + 1;
+    cur_words_ = cw;
+    if (!checkpoint_path.empty()) {
+      check(w2v_dev_download_model(dev_, W.data(), uses_C() ? C.data() : nullptr,
+                                   train_method == "hs" ? synapses1.data() : nullptr),
+            "w2v_dev_download_model");
+      checkpoint_epoch(cw, it + 1, key);
+    }
     if (verbose) {
       std::printf("\rinit_alpha: %f  Progress: %f%% ", init_alpha, 100.0 / iter * cw / train_words);
       std::fflush(stdout);
@@ -456,7 +478,6 @@ void Word2Vec::run_epochs(const std::vector<int32_t>& ids, const std::vector<int
   int64_t cw = 0;
   check(w2v_dev_get_progress(dev_, &cw), "w2v_dev_get_progress");
   cur_words_ = cw;
-  resume_ = false;
   check(w2v_dev_download_model(dev_, W.data(), uses_C() ? C.data() : nullptr,
                                train_method == "hs" ? synapses1.data() : nullptr),
         "w2v_dev_download_model");
@@ -498,7 +519,10 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
     }
   };
   try {
-    const uint64_t key = ((uint64_t)generator() << 32) | (uint64_t)generator();
+    const bool cont = resume_ && resume_epochs_ > 0 && resume_epochs_ < iter;  // as run_epochs
+    const int first = cont ? (int)resume_epochs_ : 0;
+    const uint64_t key = cont ? resume_key_ : ((uint64_t)generator() << 32) | (uint64_t)generator();
+    key_ = key;
     for (size_t i = 0; i < R; ++i) {
       cfg.device = gpu_devices[i];
       check(w2v_dev_create(&cfg, &reps[i]), "w2v_dev_create");
@@ -520,8 +544,10 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
     check(w2v_group_set_mode(grp, replica_mode), "w2v_group_set_mode");
     std::vector<long> sample_idx((size_t)n);
     std::iota(sample_idx.begin(), sample_idx.end(), 0);
-    int64_t global = resume_ ? start_words_ : 0;  // the reference's current_words over all replicas (:359, :393)
-    for (int it = 0; it < iter; ++it) {
+    int64_t global = cont ? start_words_ : 0;  // the reference's current_words over all replicas (:359, :393)
+    epochs_done_ = first;
+    resume_ = false;
+    for (int it = first; it < iter; ++it) {
       std::shuffle(sample_idx.begin(), sample_idx.end(), generator);  // :373
       // shards and their per-sentence word counts
       std::vector<std::vector<int64_t>> shard(R), cum(R);
@@ -554,13 +580,20 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
           throw std::runtime_error("word2vec_amd: training diverged on replica " + std::to_string(i) + " (" +
                                    std::to_string(st.nonfinite) + " non-finite sigma arguments)");
       }
+      epochs_done_ = it + 1;
+      cur_words_ = global;
+      if (!checkpoint_path.empty()) {
+        check(w2v_dev_download_model(reps[0], W.data(), uses_C() ? C.data() : nullptr,
+                                     train_method == "hs" ? synapses1.data() : nullptr),
+              "w2v_dev_download_model");
+        checkpoint_epoch(global, it + 1, key);
+      }
       if (verbose) {
         std::printf("\rinit_alpha: %f  Progress: %f%% ", init_alpha, 100.0 / iter * global / train_words);
         std::fflush(stdout);
       }
     }
     cur_words_ = global;
-    resume_ = false;
     check(w2v_dev_download_model(reps[0], W.data(), uses_C() ? C.data() : nullptr,
                                  train_method == "hs" ? synapses1.data() : nullptr),
           "w2v_dev_download_model");
@@ -784,16 +817,15 @@ void Word2Vec::load_word2vec(std::string filename, bool binary) {
 
 // ---------------------------------------------------------------------------
 // Checkpoints (additive; SURVEY.md §5: the reference saves only the final
-// vectors, Word2Vec.cpp:398-438). A snapshot between train() calls: W, C,
-// synapses1, the word counter (current_words, Word2Vec.cpp:359,393) and the
-// generator state, with the vocabulary's size and a hash of its words to catch
-// a mismatched resume. load_checkpoint restores them; the next train() /
-// train_ids() / train_file() then continues from the restored weights (no
-// init_weights) with current_words starting at the saved count.
+// vectors, Word2Vec.cpp:398-438): W, C, synapses1, the word counter
+// (current_words, Word2Vec.cpp:359,393), the epochs of the schedule done, the
+// iter they belong to, the Philox key and the generator state, with the
+// vocabulary's size and a hash of its words to catch a mismatched resume.
+// Semantics: include/Word2Vec.h (checkpoint_path, load_checkpoint).
 // ---------------------------------------------------------------------------
 namespace {
 
-const char kCkptMagic[8] = {'W', '2', 'V', 'C', 'K', 'P', 'T', '1'};
+const char kCkptMagic[8] = {'W', '2', 'V', 'C', 'K', 'P', 'T', '2'};
 
 uint64_t vocab_hash64(const std::vector<Word*>& vocab) {
   uint64_t h = 1469598103934665603ull;  // FNV-1a over "text\0count\0" in vocab order
@@ -813,11 +845,17 @@ void write_matrix(std::ofstream& out, const RMatrixXf& M) {
   if (r * c > 0) out.write((const char*)M.data(), (std::streamsize)(r * c * 4));
 }
 
-void read_matrix(std::ifstream& in, RMatrixXf& M) {
+// A matrix of exactly `rows` x `cols` (rows == 0: an empty matrix, any cols).
+void read_matrix(std::ifstream& in, RMatrixXf& M, int64_t rows, int64_t cols, const char* name) {
   int64_t r = 0, c = 0;
   in.read((char*)&r, 8);
   in.read((char*)&c, 8);
   if (!in || r < 0 || c < 0 || r * c > ((int64_t)1 << 40)) throw std::runtime_error("checkpoint: bad matrix header");
+  const bool ok = rows == 0 ? r * c == 0 : (r == rows && c == cols);
+  if (!ok)
+    throw std::runtime_error(std::string("checkpoint: ") + name + " is " + std::to_string(r) + " x " +
+                             std::to_string(c) + ", this object needs " + std::to_string(rows) + " x " +
+                             std::to_string(rows ? cols : 0));
   M.resize((w2v_dense::Index)r, (w2v_dense::Index)c);
   if (r * c > 0) in.read((char*)M.data(), (std::streamsize)(r * c * 4));
   if (!in) throw std::runtime_error("checkpoint: truncated matrix");
@@ -825,16 +863,17 @@ void read_matrix(std::ifstream& in, RMatrixXf& M) {
 
 }  // namespace
 
-void Word2Vec::save_checkpoint(const std::string& path) {
+void Word2Vec::write_checkpoint(const std::string& path, int64_t cw, int64_t epochs_done, uint64_t key) {
   std::ofstream out(path, std::ios::binary);
   if (!out) throw std::runtime_error("checkpoint: cannot write " + path);
   out.write(kCkptMagic, 8);
-  const int64_t V = (int64_t)vocab.size(), d = word_dim, cw = cur_words_;
+  const int64_t hdr[2] = {(int64_t)vocab.size(), (int64_t)word_dim};
   const uint64_t vh = vocab_hash64(vocab);
-  out.write((const char*)&V, 8);
-  out.write((const char*)&d, 8);
+  const int64_t pos[3] = {cw, epochs_done, (int64_t)iter};
+  out.write((const char*)hdr, 16);
   out.write((const char*)&vh, 8);
-  out.write((const char*)&cw, 8);
+  out.write((const char*)pos, 24);
+  out.write((const char*)&key, 8);
   std::ostringstream gs;
   gs << generator;
   const std::string g = gs.str();
@@ -847,30 +886,65 @@ void Word2Vec::save_checkpoint(const std::string& path) {
   if (!out) throw std::runtime_error("checkpoint: write failed for " + path);
 }
 
+// After epoch `epochs_done` of a train call (checkpoint_path set; the host
+// matrices hold that epoch's model).
+void Word2Vec::checkpoint_epoch(int64_t cw, int64_t epochs_done, uint64_t key) {
+  std::string path = checkpoint_path;
+  const size_t p = path.find("%d");
+  if (p != std::string::npos) path.replace(p, 2, std::to_string(epochs_done));
+  write_checkpoint(path, cw, epochs_done, key);
+}
+
+void Word2Vec::save_checkpoint(const std::string& path) { write_checkpoint(path, cur_words_, epochs_done_, key_); }
+
 void Word2Vec::load_checkpoint(const std::string& path) {
   std::ifstream in(path, std::ios::binary);
   if (!in) throw std::runtime_error("checkpoint: cannot read " + path);
   char magic[8];
   in.read(magic, 8);
   if (!in || std::memcmp(magic, kCkptMagic, 8) != 0) throw std::runtime_error("checkpoint: not a word2vec_amd checkpoint");
-  int64_t V = 0, d = 0, cw = 0, gl = 0;
-  uint64_t vh = 0;
+  int64_t V = 0, d = 0, cw = 0, ep = 0, it = 0, gl = 0;
+  uint64_t vh = 0, key = 0;
   in.read((char*)&V, 8);
   in.read((char*)&d, 8);
   in.read((char*)&vh, 8);
   in.read((char*)&cw, 8);
+  in.read((char*)&ep, 8);
+  in.read((char*)&it, 8);
+  in.read((char*)&key, 8);
   in.read((char*)&gl, 8);
   if (!in || V != (int64_t)vocab.size() || d != word_dim || vh != vocab_hash64(vocab))
     throw std::runtime_error("checkpoint: vocabulary or word_dim differs from this object's");
+  if (cw < 0 || ep < 0 || it < 1 || ep > it) throw std::runtime_error("checkpoint: bad schedule position");
   if (gl < 0 || gl > (1 << 20)) throw std::runtime_error("checkpoint: bad generator state");
   std::string g((size_t)gl, '\0');
   in.read(&g[0], (std::streamsize)gl);
-  std::istringstream gs(g);
-  gs >> generator;
-  read_matrix(in, W);
-  read_matrix(in, C);
-  read_matrix(in, synapses1);
+  if (!in) throw std::runtime_error("checkpoint: truncated generator state");
+  std::mt19937 gen;
+  {
+    std::istringstream gs(g);
+    gs >> gen;
+    if (!gs) throw std::runtime_error("checkpoint: bad generator state");
+  }
+  // every matrix is read into a temporary and checked against the shapes this
+  // object trains (init_weights): W V x d; C V x d when uses_C(), else empty;
+  // synapses1 (V-1) x d for hs, else empty
+  RMatrixXf w, c, s1;
+  read_matrix(in, w, V, d, "W");
+  read_matrix(in, c, uses_C() ? V : 0, d, "C");
+  read_matrix(in, s1, train_method == "hs" ? std::max<int64_t>(V - 1, 0) : 0, d, "synapses1");
+  if (V > 0 && w.rows() == 0) throw std::runtime_error("checkpoint: saved before init_weights (W is empty)");
+  // commit
+  W = std::move(w);
+  C = std::move(c);
+  synapses1 = std::move(s1);
+  generator = gen;
   cur_words_ = cw;
   start_words_ = cw;
+  epochs_done_ = ep;
+  key_ = key;
+  // a mid-schedule checkpoint of the same iter continues it (include/Word2Vec.h)
+  resume_epochs_ = it == iter ? ep : 0;
+  resume_key_ = key;
   resume_ = true;
 }

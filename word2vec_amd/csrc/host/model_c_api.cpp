@@ -260,6 +260,10 @@ int w2v_model_load_checkpoint(w2v_model* m, const char* path) {
   return guard(m, [&] { m->w.load_checkpoint(path); });
 }
 int64_t w2v_model_current_words(w2v_model* m) { return m->w.current_words(); }
+int w2v_model_set_checkpoint_path(w2v_model* m, const char* path) {
+  return guard(m, [&] { m->w.checkpoint_path = path ? path : ""; });
+}
+int64_t w2v_model_epochs_done(w2v_model* m) { return m->w.epochs_done(); }
 int w2v_model_save_vocab(w2v_model* m, const char* path) {
   return guard(m, [&] { m->w.save_vocab(path); });
 }

@@ -61,6 +61,8 @@ def _load():
             "w2v_model_save_vocab": (C.c_int, [P, S]),
             "w2v_model_save_checkpoint": (C.c_int, [P, S]),
             "w2v_model_load_checkpoint": (C.c_int, [P, S]),
+            "w2v_model_set_checkpoint_path": (C.c_int, [P, S]),
+            "w2v_model_epochs_done": (I64, [P]),
             "w2v_model_current_words": (I64, [P]),
             "w2v_model_read_vocab": (C.c_int, [P, S]),
         }
@@ -89,7 +91,7 @@ class Word2Vec:
                  train_method="hs", model="cbow", gpu_device=0, replay_rng=False, verbose=False, hot_rows=-2,
                  private_rows=-1, flush_centers=0, private_average=8.0, max_waves=0, shared_negatives=False,
                  context_rows=-1, context_flush=0, gpu_devices=None, sync_words=0, overlap_average=True,
-                 gpu_ingest=False, ingest_chunk_bytes=0):
+                 gpu_ingest=False, ingest_chunk_bytes=0, checkpoint_path=""):
         self.L = _load()
         self.word_dim = word_dim
         self.h = self.L.w2v_model_new(iter, window, min_count, table_size, word_dim, negative, subsample_threshold,
@@ -106,6 +108,8 @@ class Word2Vec:
             devs = np.ascontiguousarray(gpu_devices, np.int32)
             self.L.w2v_model_replicas(self.h, _p(devs), devs.size, int(sync_words), int(bool(overlap_average)))
         self.L.w2v_model_set_gpu_ingest(self.h, int(bool(gpu_ingest)), int(ingest_chunk_bytes))
+        if checkpoint_path:
+            self.set_checkpoint_path(checkpoint_path)
 
     def __del__(self):
         try:
@@ -187,8 +191,18 @@ class Word2Vec:
         self._chk(self.L.w2v_model_save_checkpoint(self.h, str(path).encode()), "save_checkpoint")
 
     def load_checkpoint(self, path):
-        """Restore W / C / synapses1, current_words and the generator; the next train continues from them."""
+        """Restore W / C / synapses1, current_words, the schedule position and the generator: a mid-schedule
+        checkpoint's next train runs the remaining epochs, a whole-schedule one starts a new schedule on the
+        loaded weights (include/Word2Vec.h)."""
         self._chk(self.L.w2v_model_load_checkpoint(self.h, str(path).encode()), "load_checkpoint")
+
+    def set_checkpoint_path(self, path):
+        """Write a checkpoint after every epoch of train ("" = off; "%d" in the path = the epochs done)."""
+        self._chk(self.L.w2v_model_set_checkpoint_path(self.h, str(path).encode()), "set_checkpoint_path")
+
+    @property
+    def epochs_done(self) -> int:
+        return self.L.w2v_model_epochs_done(self.h)
 
     @property
     def current_words(self) -> int:
