@@ -312,7 +312,10 @@ typedef struct w2v_group w2v_group;
 int w2v_group_unique_id(uint8_t* id /* W2V_GROUP_ID_BYTES */);
 /* members: the n handles this process drives (same model shape). unique_id
  * NULL: all replicas are in this process (nranks = n). Otherwise this
- * process's replicas are ranks [first_rank, first_rank + n) of nranks. */
+ * process's replicas are ranks [first_rank, first_rank + n) of nranks; with a
+ * unique id even nranks = 1 builds the RCCL communicator and runs every
+ * round's delta -> ncclAllReduce -> fold (the model is unchanged by it: the
+ * sum of one replica's deltas), so one GPU exercises the exchange path. */
 int w2v_group_create(w2v_dev** members, int32_t n, const uint8_t* unique_id, int32_t nranks, int32_t first_rank,
                      w2v_group** out);
 void w2v_group_destroy(w2v_group* g);

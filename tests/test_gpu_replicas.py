@@ -1,7 +1,9 @@
 """Data-parallel replicas on the GPU (include/w2v_dev.h w2v_group_*, SURVEY.md
 §8(e)). The box has one GPU, so the replicas share it: the group averages them
-with its same-device kernel (RCCL cannot put two ranks on one GPU; the RCCL
-path runs in the driver's multi-GPU bench). Checked here: the average is the
+with its same-device kernel (RCCL cannot put two ranks on one GPU: "Duplicate
+GPU detected"). The RCCL path itself (ncclCommInitRank, the grouped
+ncclAllReduce on the communication stream, the fold) runs here on a ONE-rank
+communicator (test_rccl_exchange_one_rank). Checked here: the average is the
 exact element-wise mean, blocking and overlapped; an epoch cut into order
 slices trains what one launch over the epoch trains; and the C++ class with
 two replicas on one device (gpu_devices = {0, 0}) lands within a point of a
@@ -74,6 +76,45 @@ def test_group_exchange(mode, overlap, gmode):
     g.close()
     for d in ds:
         d.close()
+
+
+@pytest.mark.parametrize("gmode", ["sum", "row_average", "average"])
+@pytest.mark.parametrize("overlap", [False, True])
+def test_rccl_exchange_one_rank(overlap, gmode):
+    """The RCCL exchange path on one GPU: a group built from a unique id with
+    nranks = 1 (ncclCommInitRank) runs every round's delta kernel, the grouped
+    in-place ncclAllReduce (on the communication stream when overlapped) and
+    the fold. With one rank the all-reduced sum is the replica's own delta, so
+    the exchange must leave the model bit-identical: a replica trained in 5
+    rounds with an exchange after each equals the same rounds without a group
+    (one wavefront, deterministic), and the exchange counter advances."""
+    from word2vec_amd.replicas import group_unique_id
+
+    o, (a, b) = _pair_of_handles("cbow_hs" if gmode == "row_average" else "sg_ns")
+    n = o.samples()[1].size - 1
+    order = np.random.default_rng(9).permutation(n)
+    for d in (a, b):
+        d.set_rng(N.W2V_RNG_PHILOX, 91)
+        d.set_schedule(N.W2V_SCHED_SEQUENTIAL)
+        d.set_progress(0)
+        d.set_order(order)
+    g = NativeAverager([b], unique_id=group_unique_id(), nranks=1, overlap=overlap, mode=gmode)
+    info = g.info()
+    assert info["nranks"] == 1 and not info["local"] and info["overlap"] == overlap
+    step = (n + 4) // 5
+    for lo in range(0, n, step):
+        a.train_slice_async(0, lo, min(step, n - lo))
+        b.train_slice_async(0, lo, min(step, n - lo))
+        g.average()
+    g.finish()
+    a.synchronize()
+    assert g.info()["rounds"] == (n + step - 1) // step
+    for x, y in zip(a.download_model(), b.download_model()):
+        if x is not None:
+            np.testing.assert_array_equal(x, y)
+    g.close()
+    a.close()
+    b.close()
 
 
 def test_order_slices_equal_one_launch():

@@ -158,6 +158,8 @@ struct w2v_group {
   std::vector<Member> m;
   int nranks = 1;
   bool local = false;       // every replica in this process, on one device: summing kernels, no RCCL
+  bool exchange = false;    // rounds exchange anything: > 1 rank, or a communicator was asked for (unique id;
+                            // one rank still runs the full RCCL round trip, which is how one GPU tests it)
   bool overlap = false;
   int32_t mode = W2V_GROUP_SUM;
   int64_t pitch = 0;
@@ -335,6 +337,7 @@ int w2v_group_create(w2v_dev** members, int32_t n, const uint8_t* unique_id, int
   bool same = true;
   for (auto& x : g->m) same = same && x.device == g->m[0].device;
   g->local = n > 1 && same && !unique_id;
+  g->exchange = nranks > 1 || unique_id != nullptr;
   for (size_t i = 0; i < g->m.size(); ++i) {
     Member& x = g->m[i];
     bool ok = hipSetDevice(x.device) == hipSuccess &&
@@ -342,7 +345,7 @@ int w2v_group_create(w2v_dev** members, int32_t n, const uint8_t* unique_id, int
               hipEventCreateWithFlags(&x.ready, hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&x.done, hipEventDisableTiming) == hipSuccess;
     // P (the shared model: every replica starts from the same weights), D, A
-    for (int k = 0; k < 3 && ok && nranks > 1; ++k) {
+    for (int k = 0; k < 3 && ok && g->exchange; ++k) {
       if (!g->elems[k]) continue;
       const size_t bytes = (size_t)g->elems[k] * sizeof(float);
       const size_t fbytes = (size_t)((g->elems[k] / g->pitch + 3) & ~int64_t(3)) * sizeof(float);  // rows, float4-padded
@@ -358,7 +361,7 @@ int w2v_group_create(w2v_dev** members, int32_t n, const uint8_t* unique_id, int
       return fail_g(W2V_ERR_HIP, "w2v_group_create: stream / event / exchange buffer setup failed (out of memory?)");
     }
   }
-  if (!g->local && nranks > 1) {
+  if (!g->local && g->exchange) {
     ncclResult_t r = ncclSuccess;
     if (!unique_id) {
       std::vector<int> devs;
@@ -417,7 +420,7 @@ int w2v_group_set_mode(w2v_group* g, int32_t mode) {
 int w2v_group_average_async(w2v_group* g) {
   w2v::Range range_("w2v_group_average_async");
   if (!g) return fail_g(W2V_ERR_ARG, "null group");
-  if (g->nranks == 1) return W2V_OK;
+  if (!g->exchange) return W2V_OK;
   ++g->rounds;
   // extract this round's deltas (and fold the pending exchange in, overlap)
   const bool fold = g->overlap && g->pending;
