@@ -176,8 +176,12 @@ class Word2Vec {
   uint64_t resume_key_ = 0;         //   ... with this Philox key
   int64_t epochs_done_ = 0;         // epochs of the last train call's schedule completed
   uint64_t key_ = 0;                // Philox key of the last train call
+  std::string sched_gen_;           // generator state at the start of the last train call's schedule
+  std::string resume_sched_gen_;    // ... of the checkpoint's schedule (replayed to continue it)
   void write_checkpoint(const std::string& path, int64_t cw, int64_t epochs_done, uint64_t key);
   void checkpoint_epoch(int64_t cw, int64_t epochs_done, uint64_t key);
+  std::string generator_state() const;
+  void restore_generator(const std::string& state);
   w2v_ingest* ingest_ = nullptr;    // gpu_ingest: the counted file ...
   std::string ingest_key_;          //   ... (path + format)
   std::vector<std::string> ingest_words_;  // its distinct words, in order of first occurrence

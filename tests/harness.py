@@ -81,3 +81,34 @@ def elem_rel_err(a, b, floor_frac=1e-3):
 def errs(a, b):
     """(norm-wise, per-element) relative error, for messages and logs."""
     return rel_err(a, b), elem_rel_err(a, b)
+
+
+def check_parity(got, want, init, norm_tol, elem_tol, tag=""):
+    """Assert both bounds on every matrix's update (got - init vs want - init):
+    norm-wise rel_err < norm_tol AND per-element elem_rel_err < elem_tol; a
+    matrix the oracle left untouched must come back bit-identical. Each
+    measurement is printed and, with W2V_PARITY_LOG=<file>, appended to it as
+    a JSON line (the measured errors the bounds in the tests come from)."""
+    import json
+    import os
+
+    out = []
+    for k, (g, w, i) in enumerate(zip(got, want, init)):
+        if w is None:
+            continue
+        dw = np.asarray(w, np.float64) - i
+        if np.abs(dw).max() == 0:
+            np.testing.assert_array_equal(g, w)
+            continue
+        en, ee = errs(np.asarray(g, np.float64) - i, dw)
+        out.append((k, en, ee))
+        print(f"{tag} matrix {k}: rel_err {en:.2e} elem_rel_err {ee:.2e}")
+        path = os.environ.get("W2V_PARITY_LOG")
+        if path:
+            with open(path, "a") as f:
+                f.write(json.dumps({"tag": tag, "matrix": k, "rel_err": en, "elem_rel_err": ee,
+                                    "norm_tol": norm_tol, "elem_tol": elem_tol}) + "\n")
+    for k, en, ee in out:
+        assert en < norm_tol, (tag, k, en, norm_tol)
+        assert ee < elem_tol, (tag, k, ee, elem_tol)
+    return out

@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Replica-exchange quality study on ONE GPU (VERDICT r02 "next" 1).
+
+R replicas (R DeviceTrainer handles on cuda:0, one same-device w2v_group) each
+train a contiguous shard of every epoch's shuffled sentence order at full
+concurrency and exchange their updates every 1/rounds of an epoch (SUM,
+AVERAGE or ROW_AVERAGE; blocking or overlapped), exactly as bench.py --gpus R
+and Word2Vec::gpu_devices do across GPUs. Compared against ONE replica that
+trains every sentence, at equal tokens, on a planted-relation Zipf corpus
+(the text8-like gate corpus of tests/quality.py, scaled up, generated as ids
+with numpy). Output: one JSON line per run (analogy, similarity, delta to the
+single replica of the same seed).
+
+usage: replica_study.py [--tokens N] [--replicas 8] [--rounds 1,8,32,128]
+                        [--gmodes sum,average,row_average] [--seeds 1,2]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT))
+
+from word2vec_amd import _native as N  # noqa: E402
+from word2vec_amd import host  # noqa: E402
+from word2vec_amd.device import Config, DeviceTrainer  # noqa: E402
+from word2vec_amd.replicas import NativeAverager  # noqa: E402
+
+
+def planted_zipf_ids(n_tokens, sent_len=1000, filler=100_000, rows=50, cols=4, topic=8, role=8, planted_frac=0.10,
+                     seed=0):
+    """tests/quality.py planted_zipf_corpus as raw ids (vectorised): filler ids
+    [0, filler), entities, topics, roles after it."""
+    rng = np.random.default_rng(seed)
+    n_sent = n_tokens // sent_len
+    E0 = filler
+    T0 = E0 + rows * cols
+    R0 = T0 + rows * topic
+    n_raw = R0 + cols * role
+    p = 1.0 / np.arange(1, filler + 1)
+    cdf = np.cumsum(p)
+    cdf /= cdf[-1]
+    tok = np.searchsorted(cdf, rng.random(n_sent * sent_len), side="right").clip(0, filler - 1).astype(np.int64)
+    si = rng.integers(rows, size=n_sent)
+    sj = rng.integers(cols, size=n_sent)
+    pos = np.flatnonzero(rng.random(n_sent * sent_len) < planted_frac)
+    s = pos // sent_len
+    i, j = si[s], sj[s]
+    kind = rng.random(pos.size)
+    ent = kind < 0.34
+    top = (kind >= 0.34) & (kind < 0.67)
+    rol = kind >= 0.67
+    # entity: the sentence's (i, j) w.p. 0.75, else a same-row or same-column neighbour
+    r1 = rng.random(pos.size)
+    r2 = rng.random(pos.size)
+    ei, ej = i.copy(), j.copy()
+    cross = r1 <= 0.25
+    rowx = cross & (r2 < 0.5)
+    colx = cross & (r2 >= 0.5)
+    ej[rowx] = rng.integers(cols, size=int(rowx.sum()))
+    ei[colx] = rng.integers(rows, size=int(colx.sum()))
+    out = np.empty(pos.size, np.int64)
+    out[ent] = E0 + ei[ent] * cols + ej[ent]
+    out[top] = T0 + i[top] * topic + rng.integers(topic, size=int(top.sum()))
+    out[rol] = R0 + j[rol] * role + rng.integers(role, size=int(rol.sum()))
+    tok[pos] = out
+    names = ([f"f{k}" for k in range(filler)] + [f"e{a}_{b}" for a in range(rows) for b in range(cols)]
+             + [f"t{a}_{k}" for a in range(rows) for k in range(topic)]
+             + [f"r{b}_{k}" for b in range(cols) for k in range(role)])
+    assert len(names) == n_raw
+    qs = [(f"e{a}_{l}", f"e{a}_{b}", f"e{c}_{l}", f"e{c}_{b}") for a in range(rows) for c in range(rows) if a != c
+          for b in range(cols) for l in range(cols) if b != l]
+    prs = []
+    for a in range(rows):
+        for b in range(cols):
+            for c in range(rows):
+                for d in range(cols):
+                    if (a, b) < (c, d) and rng.random() < 0.05:
+                        prs.append((f"e{a}_{b}", f"e{c}_{d}", float((a == c) + (b == d))))
+    return tok, n_sent, names, qs, prs
+
+
+def build(tok, n_sent, sent_len, names, min_count=5):
+    counts = np.bincount(tok, minlength=len(names))
+    order = np.argsort(-counts, kind="stable")
+    V = int((counts >= min_count).sum())
+    vr = order[:V]
+    remap = np.full(len(names), -1, np.int64)
+    remap[vr] = np.arange(V)
+    ids = remap[tok]
+    keep = ids >= 0
+    lens = keep.reshape(n_sent, sent_len).sum(1)
+    soff = np.zeros(n_sent + 1, np.int64)
+    soff[1:] = np.cumsum(lens)
+    return ids[keep].astype(np.int32), soff, counts[vr].astype(np.int64), [names[k] for k in vr]
+
+
+def gpu_scores(words, E, qs, prs, dev):
+    idx = {w: k for k, w in enumerate(words)}
+    En = torch.tensor(E, device=dev)
+    En = En / En.norm(dim=1, keepdim=True).clamp_min(1e-12)
+    Q = torch.tensor([[idx[x] for x in q] for q in qs if all(x in idx for x in q)], device=dev)
+    correct = 0
+    for s in range(0, Q.shape[0], 4096):
+        qa, qb, qc, qd = Q[s:s + 4096].T
+        sims = (En[qb] - En[qa] + En[qc]) @ En.T
+        r = torch.arange(qa.numel(), device=dev)
+        for ex in (qa, qb, qc):
+            sims[r, ex] = -float("inf")
+        correct += int((sims.argmax(1) == qd).sum())
+    from word2vec_amd.evaluate import similarity_score
+
+    return 100.0 * correct / max(1, Q.shape[0]), similarity_score(words, E, prs)["spearman"]
+
+
+def train(args, R, rounds, gmode, overlap, seed, data, dev):
+    ids, soff, counts, words, mode = data
+    n = soff.size - 1
+    hs = mode == "cbow_hs"
+    cbow = mode.startswith("cbow")
+    neg = 0 if hs else 5
+    keep = host.sample_probs(counts, 1e-4)
+    bounds = host.table_bounds(counts, 100_000_000) if neg else None
+    codes = points = coff = None
+    if hs:
+        codes, points, coff = host.huffman(counts)
+    V, d = counts.size, args.dim
+    rng = np.random.default_rng(seed)
+    W0 = ((rng.random((V, d), dtype=np.float32) - 0.5) / d).astype(np.float32)
+    C0 = ((rng.random((V, d), dtype=np.float32) - 0.5) / d).astype(np.float32) if hs else \
+        (np.zeros((V, d), np.float32) if (neg or cbow) else None)
+    S0 = np.zeros((V - 1, d), np.float32) if hs else None
+    cfg = Config(word_dim=d, window=5, negative=neg, hs=hs, cbow=cbow, cbow_mean=True, iter=args.iters,
+                 init_alpha=0.05 if cbow else 0.025, min_alpha=2.5e-6, table_size=100_000_000, device=0)
+    reps = []
+    for _ in range(R):
+        t = DeviceTrainer(cfg)
+        t.upload_vocab(keep, bounds, codes, points, coff)
+        t.upload_model(W0, C0, S0)
+        t.upload_corpus(ids, soff, int(args.raw_tokens))
+        t.set_train_words(max(1, int(args.raw_tokens) // R))
+        t.set_rng(N.W2V_RNG_PHILOX, (seed << 32) | 0x5EED)
+        t.set_schedule(N.W2V_SCHED_PARALLEL)
+        reps.append(t)
+    g = NativeAverager(reps, overlap=overlap, mode=gmode) if R > 1 else None
+    lens = np.diff(soff)
+    glob = 0
+    t0 = time.time()
+    for ep in range(args.iters):
+        order = np.random.default_rng(1000 * seed + ep).permutation(n).astype(np.int64)
+        shards = [order[n * i // R: n * (i + 1) // R] for i in range(R)]
+        cums = []
+        for t, sh in zip(reps, shards):
+            t.set_order(sh)
+            cums.append(np.concatenate([[0], np.cumsum(lens[sh])]))
+        for r in range(rounds):
+            words_r = 0
+            for t, sh, cu in zip(reps, shards, cums):
+                m = sh.size
+                lo, hi = m * r // rounds, m * (r + 1) // rounds
+                t.set_progress_async(glob // R)
+                if hi > lo:
+                    t.train_slice_async(ep, lo, hi - lo)
+                words_r += int(cu[hi] - cu[lo])
+            if g is not None:
+                g.average()
+            glob += words_r
+        if g is not None:
+            g.finish()
+        for t in reps:
+            t.synchronize()
+    dt = time.time() - t0
+    Wf, Cf, _ = reps[0].download_model()
+    for t in reps:
+        st = t.read_stats()
+        assert st["nonfinite"] == 0
+    if g is not None:
+        g.close()
+    for t in reps:
+        t.close()
+    return (Cf if hs else Wf), dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tokens", type=int, default=50_000_000)
+    ap.add_argument("--filler", type=int, default=200_000)
+    ap.add_argument("--dim", type=int, default=100)
+    ap.add_argument("--iters", type=int, default=1)
+    ap.add_argument("--mode", default="sg_ns")
+    ap.add_argument("--replicas", default="8")
+    ap.add_argument("--rounds", default="1,8,32,128")
+    ap.add_argument("--gmodes", default="sum,average,row_average")
+    ap.add_argument("--overlap", type=int, default=1)
+    ap.add_argument("--seeds", default="1")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    t0 = time.time()
+    tok, n_sent, names, qs, prs = planted_zipf_ids(args.tokens, filler=args.filler, seed=0)
+    args.raw_tokens = tok.size
+    ids, soff, counts, words = build(tok, n_sent, 1000, names)
+    del tok
+    print(json.dumps({"corpus_tokens": int(args.raw_tokens), "in_vocab": int(ids.size), "V": int(counts.size),
+                      "sentences": int(n_sent), "gen_s": round(time.time() - t0, 1), "mode": args.mode,
+                      "dim": args.dim, "iters": args.iters}), flush=True)
+    data = (ids, soff, counts, words, args.mode)
+    for seed in [int(s) for s in args.seeds.split(",")]:
+        E, dt = train(args, 1, 1, "sum", False, seed, data, dev)
+        a1, s1 = gpu_scores(words, E, qs, prs, dev)
+        print(json.dumps({"seed": seed, "R": 1, "analogy": round(a1, 2), "similarity": round(s1, 2),
+                          "train_s": round(dt, 2)}), flush=True)
+        for R in [int(x) for x in args.replicas.split(",")]:
+            for rounds in [int(x) for x in args.rounds.split(",")]:
+                for gm in args.gmodes.split(","):
+                    E, dt = train(args, R, rounds, gm, bool(args.overlap), seed, data, dev)
+                    a, s = gpu_scores(words, E, qs, prs, dev)
+                    print(json.dumps({"seed": seed, "R": R, "rounds_per_epoch": rounds, "gmode": gm,
+                                      "overlap": bool(args.overlap), "analogy": round(a, 2),
+                                      "similarity": round(s, 2), "d_analogy": round(a - a1, 2),
+                                      "d_similarity": round(s - s1, 2), "train_s": round(dt, 2)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

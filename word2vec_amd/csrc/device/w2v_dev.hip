@@ -870,17 +870,17 @@ static std::pair<int64_t, int64_t> private_by_rate(w2v_dev* h, double mu) {
 // read-modify-write; profiles/r02c_*). Returns {W / C rows, nodes}.
 // The W / C threshold when hot_tau_rows is 0 (the default): by the average
 // number of a row's updates in flight, rho = waves x (window + 1) / V. A large
-// vocabulary (rho <= 1: configs[2] 0.033, configs[0] 0.2, the text8-like
-// gate corpus 0.5) takes 4: the rows between 1 and 4 expected updates in
-// flight (about a tenth of the update mass under Zipf) race rarely enough for
-// plain read-modify-write, and 1738 -> 435 atomic rows run configs[2] 11 %
-// faster with the text8-like paired scores unchanged
-// (profiles/r02z_hot_tau_probe.log). A small one (the planted corpus, V =
-// 3.4K: rho 14; text8_small, V = 20K: 2.4) keeps 1: at 4 the planted SG-HS
-// center rows fell to plain read-modify-write and the run collapsed
-// (analogy 6 vs 89, profiles/r02c_*). The shared-negatives kernel keeps 1
-// (its floor of 1000 atomic rows decides there).
-constexpr double kHotTauLargeV = 4.0, kHotTauSmallV = 1.0, kHotRhoLargeV = 1.0;
+// vocabulary (rho <= 0.1: configs[2] 0.033) takes 4: the rows between 1 and 4
+// expected updates in flight race rarely enough for plain read-modify-write,
+// and 1738 -> 435 atomic rows run configs[2] 2-11 % faster, box to box
+// (profiles/r03a_hot_tau.log, r02z_hot_tau_probe.log). A smaller one keeps 1:
+// configs[0] (rho 0.2) gains 1-2 %, the text8-like gate corpus (rho 0.5) lost
+// up to 2.6 similarity points at 4 (one seed of three at -0.9 vs the oracle,
+// r03a), and at 4 the planted SG-HS run (V = 3.4K, rho 14) collapsed: its
+// center rows fell to plain read-modify-write (analogy 6 vs 89,
+// profiles/r02c_*). The shared-negatives kernel keeps 1 (its floor of 1000
+// atomic rows decides there).
+constexpr double kHotTauLargeV = 4.0, kHotTauSmallV = 1.0, kHotRhoLargeV = 0.1;
 static double hot_tau_for(const w2v_dev* h, double waves, bool shared) {
   if (h->hot_tau_rows > 0.0) return h->hot_tau_rows;
   if (shared || h->V <= 0) return kHotTauSmallV;

@@ -431,10 +431,16 @@ void Word2Vec::run_epochs(const std::vector<int32_t>& ids, const std::vector<int
   std::iota(sample_idx.begin(), sample_idx.end(), 0);
   std::vector<std::vector<int64_t>> orders((size_t)iter);
   uint64_t key = 0;
+  if (!replay_rng) key = cont ? resume_key_ : ((uint64_t)generator() << 32) | (uint64_t)generator();
+  // the schedule's shuffles are cumulative (each epoch shuffles the previous
+  // order) and the replay stream follows them: continuing replays the whole
+  // schedule's generator from its start and trains the remaining epochs
+  if (cont) restore_generator(resume_sched_gen_);
+  sched_gen_ = generator_state();
   if (replay_rng) {
     std::vector<uint32_t> stream;
     std::vector<int64_t> stream_off((size_t)(n * iter), 0);
-    for (int it = first; it < iter; ++it) {
+    for (int it = 0; it < iter; ++it) {
       std::shuffle(sample_idx.begin(), sample_idx.end(), generator);
       orders[(size_t)it].assign(sample_idx.begin(), sample_idx.end());
       append_reference_draws(ids, offsets, sample_idx, stream, stream_off, it);
@@ -445,18 +451,18 @@ void Word2Vec::run_epochs(const std::vector<int32_t>& ids, const std::vector<int
     check(w2v_dev_set_rng(dev_, W2V_RNG_REPLAY, 0), "w2v_dev_set_rng");
     check(w2v_dev_set_schedule(dev_, W2V_SCHED_SEQUENTIAL), "w2v_dev_set_schedule");
   } else {
-    key = cont ? resume_key_ : ((uint64_t)generator() << 32) | (uint64_t)generator();
     check(w2v_dev_set_rng(dev_, W2V_RNG_PHILOX, key), "w2v_dev_set_rng");
     check(w2v_dev_set_schedule(dev_, W2V_SCHED_PARALLEL), "w2v_dev_set_schedule");
   }
   key_ = key;
   epochs_done_ = first;
   resume_ = false;
-  for (int it = first; it < iter; ++it) {
+  for (int it = 0; it < iter; ++it) {
     if (!replay_rng) {
       std::shuffle(sample_idx.begin(), sample_idx.end(), generator);
       orders[(size_t)it].assign(sample_idx.begin(), sample_idx.end());
     }
+    if (it < first) continue;  // done before the checkpoint
     w2v_dev_stats st;
     std::memset(&st, 0, sizeof(st));
     check(w2v_dev_train_epoch(dev_, it, orders[(size_t)it].data(), &st), "w2v_dev_train_epoch");
@@ -523,6 +529,8 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
     const int first = cont ? (int)resume_epochs_ : 0;
     const uint64_t key = cont ? resume_key_ : ((uint64_t)generator() << 32) | (uint64_t)generator();
     key_ = key;
+    if (cont) restore_generator(resume_sched_gen_);  // as run_epochs: replay the schedule's shuffles
+    sched_gen_ = generator_state();
     for (size_t i = 0; i < R; ++i) {
       cfg.device = gpu_devices[i];
       check(w2v_dev_create(&cfg, &reps[i]), "w2v_dev_create");
@@ -547,8 +555,9 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
     int64_t global = cont ? start_words_ : 0;  // the reference's current_words over all replicas (:359, :393)
     epochs_done_ = first;
     resume_ = false;
-    for (int it = first; it < iter; ++it) {
+    for (int it = 0; it < iter; ++it) {
       std::shuffle(sample_idx.begin(), sample_idx.end(), generator);  // :373
+      if (it < first) continue;  // done before the checkpoint
       // shards and their per-sentence word counts
       std::vector<std::vector<int64_t>> shard(R), cum(R);
       int64_t largest = 0;
@@ -874,12 +883,11 @@ void Word2Vec::write_checkpoint(const std::string& path, int64_t cw, int64_t epo
   out.write((const char*)&vh, 8);
   out.write((const char*)pos, 24);
   out.write((const char*)&key, 8);
-  std::ostringstream gs;
-  gs << generator;
-  const std::string g = gs.str();
-  const int64_t gl = (int64_t)g.size();
-  out.write((const char*)&gl, 8);
-  out.write(g.data(), (std::streamsize)gl);
+  for (const std::string& g : {generator_state(), sched_gen_}) {
+    const int64_t gl = (int64_t)g.size();
+    out.write((const char*)&gl, 8);
+    out.write(g.data(), (std::streamsize)gl);
+  }
   write_matrix(out, W);
   write_matrix(out, C);
   write_matrix(out, synapses1);
@@ -893,6 +901,18 @@ void Word2Vec::checkpoint_epoch(int64_t cw, int64_t epochs_done, uint64_t key) {
   const size_t p = path.find("%d");
   if (p != std::string::npos) path.replace(p, 2, std::to_string(epochs_done));
   write_checkpoint(path, cw, epochs_done, key);
+}
+
+std::string Word2Vec::generator_state() const {
+  std::ostringstream gs;
+  gs << generator;
+  return gs.str();
+}
+
+void Word2Vec::restore_generator(const std::string& state) {
+  std::istringstream gs(state);
+  gs >> generator;
+  if (!gs) throw std::runtime_error("word2vec_amd: bad saved generator state");
 }
 
 void Word2Vec::save_checkpoint(const std::string& path) { write_checkpoint(path, cur_words_, epochs_done_, key_); }
@@ -912,19 +932,24 @@ void Word2Vec::load_checkpoint(const std::string& path) {
   in.read((char*)&ep, 8);
   in.read((char*)&it, 8);
   in.read((char*)&key, 8);
-  in.read((char*)&gl, 8);
   if (!in || V != (int64_t)vocab.size() || d != word_dim || vh != vocab_hash64(vocab))
     throw std::runtime_error("checkpoint: vocabulary or word_dim differs from this object's");
   if (cw < 0 || ep < 0 || it < 1 || ep > it) throw std::runtime_error("checkpoint: bad schedule position");
-  if (gl < 0 || gl > (1 << 20)) throw std::runtime_error("checkpoint: bad generator state");
-  std::string g((size_t)gl, '\0');
-  in.read(&g[0], (std::streamsize)gl);
-  if (!in) throw std::runtime_error("checkpoint: truncated generator state");
+  std::string gstate[2];  // the generator now, and at the start of the checkpoint's schedule
   std::mt19937 gen;
-  {
-    std::istringstream gs(g);
+  for (int k = 0; k < 2; ++k) {
+    in.read((char*)&gl, 8);
+    if (!in || gl < 0 || gl > (1 << 20)) throw std::runtime_error("checkpoint: bad generator state");
+    gstate[k].assign((size_t)gl, '\0');
+    if (gl > 0) in.read(&gstate[k][0], (std::streamsize)gl);
+    if (k == 1 && gl == 0 && in) continue;  // saved before any train call: no schedule yet
+    std::istringstream gs(gstate[k]);
     gs >> gen;
-    if (!gs) throw std::runtime_error("checkpoint: bad generator state");
+    if (!in || !gs) throw std::runtime_error("checkpoint: bad generator state");
+  }
+  {
+    std::istringstream gs(gstate[0]);
+    gs >> gen;
   }
   // every matrix is read into a temporary and checked against the shapes this
   // object trains (init_weights): W V x d; C V x d when uses_C(), else empty;
@@ -946,5 +971,7 @@ void Word2Vec::load_checkpoint(const std::string& path) {
   // a mid-schedule checkpoint of the same iter continues it (include/Word2Vec.h)
   resume_epochs_ = it == iter ? ep : 0;
   resume_key_ = key;
+  resume_sched_gen_ = gstate[1];
+  sched_gen_ = gstate[1];
   resume_ = true;
 }
