@@ -189,6 +189,7 @@ class Word2Vec {
   void ingest_count(const std::string& path, const std::string& format);
 
   bool uses_C() const;
+  void check_limits() const;
   void finish_vocab(std::unordered_map<std::string, int>& tally);
   void ensure_device();
   void upload_vocab_products();

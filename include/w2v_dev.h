@@ -94,6 +94,15 @@ const char* w2v_dev_last_error(void); /* thread-local message of the last failur
  * set). They are read once there, never per launch. */
 const char* w2v_dev_knobs(w2v_dev* h);
 
+/* The kernels' range of the reference's unbounded hyper-parameters
+ * (Word2Vec.cpp:254, 285, 335 accept any window / negative): word_dim <= 1024,
+ * window <= 127, negative <= 63 (w2v_dev_create returns W2V_ERR_UNSUPPORTED
+ * beyond them); the shared-negatives update: window <= 8, negative <= 15.
+ * Callers check these up front (Word2Vec::train, the CLI) to fail before any
+ * corpus work, naming the reference's member / flag. Any pointer may be NULL. */
+int w2v_dev_limits(int32_t* max_dim, int32_t* max_window, int32_t* max_negative, int32_t* shared_max_window,
+                   int32_t* shared_max_negative);
+
 /* Replaces: the Word2Vec ctor's device-relevant state (Word2Vec.cpp:12-17). */
 int w2v_dev_create(const w2v_dev_config* cfg, w2v_dev** out);
 void w2v_dev_destroy(w2v_dev* h);

@@ -215,3 +215,44 @@ def test_checkpoint_load_rejects_bad_shapes(tmp_path):
     with _pytest.raises(RuntimeError, match="checkpoint"):
         hs.load_checkpoint(tmp_path / "ns.bin")
     np.testing.assert_array_equal(hs.matrix(0), before)
+
+
+def test_hyperparameter_limits_fail_early():
+    """The reference accepts any window / negative / word_dim
+    (Word2Vec.cpp:254, 285, 335); the GPU kernels' range (w2v_dev_limits) is
+    enforced before any corpus or device work: the class names the member, the
+    CLI the reference's flag."""
+    import ctypes as C
+
+    import pytest
+
+    from tests.corpus import zipf_sentences
+    from word2vec_amd import _native as N
+    from word2vec_amd.model import Word2Vec
+
+    lib = N.load_dev_lib()
+    v = [C.c_int32() for _ in range(5)]
+    assert lib.w2v_dev_limits(*[C.byref(x) for x in v]) == 0
+    assert [x.value for x in v] == [1024, 127, 63, 8, 15]
+    sents = zipf_sentences(5, 50, 100, seed=1)
+    for kw, what in ((dict(window=128), "window"), (dict(negative=64), "negative"), (dict(word_dim=1025), "word_dim")):
+        base = dict(iter=1, window=5, min_count=1, table_size=1000, word_dim=16, negative=5, train_method="ns",
+                    model="sg")
+        base.update(kw)
+        w = Word2Vec(**base)
+        w.build_vocab(sents)
+        with pytest.raises(RuntimeError, match=what):
+            w.train(sents)
+    w = Word2Vec(iter=1, window=9, min_count=1, table_size=1000, word_dim=16, negative=5, train_method="ns",
+                 model="sg", shared_negatives=True)
+    w.build_vocab(sents)
+    with pytest.raises(RuntimeError, match="shared_negatives"):
+        w.train(sents)
+    r = _cli("-window", "128", "-negative", "5")
+    assert r.returncode == 1 and "Please set -window in [0, 127]" in r.stdout
+    r = _cli("-negative", "64")
+    assert r.returncode == 1 and "Please set -negative <= 63" in r.stdout
+    r = _cli("-size", "2000", "-negative", "5")
+    assert r.returncode == 1 and "Please set -size in [1, 1024]" in r.stdout
+    r = _cli("-negative", "16", "-shared-negatives", "1")
+    assert r.returncode == 1 and "-shared-negatives 1" in r.stdout

@@ -279,14 +279,28 @@ const char* w2v_dev_last_error(void) { return g_err.c_str(); }
 
 const char* w2v_dev_knobs(w2v_dev* h) { return h ? h->knobs.desc.c_str() : ""; }
 
+// The per-pair kernels' range: a row is <= 16 floats per lane, a CBOW window
+// span is held <= 4 positions per lane, a context's negatives one per lane.
+constexpr int32_t kMaxDim = 1024, kMaxNegative = 63;
+
+int w2v_dev_limits(int32_t* max_dim, int32_t* max_window, int32_t* max_negative, int32_t* shared_max_window,
+                   int32_t* shared_max_negative) {
+  if (max_dim) *max_dim = kMaxDim;
+  if (max_window) *max_window = w2v::kMaxWindow;
+  if (max_negative) *max_negative = kMaxNegative;
+  if (shared_max_window) *shared_max_window = 8;
+  if (shared_max_negative) *shared_max_negative = 15;
+  return W2V_OK;
+}
+
 int w2v_dev_create(const w2v_dev_config* cfg, w2v_dev** out) {
   if (!cfg || !out) return fail(W2V_ERR_ARG, "w2v_dev_create: null argument");
   *out = nullptr;
   if (cfg->word_dim <= 0) return fail(W2V_ERR_ARG, "word_dim must be > 0");
-  if (cfg->word_dim > 1024) return fail(W2V_ERR_UNSUPPORTED, "word_dim > 1024 unsupported");
+  if (cfg->word_dim > kMaxDim) return fail(W2V_ERR_UNSUPPORTED, "word_dim > 1024 unsupported");
   if (cfg->window < 0 || cfg->window > w2v::kMaxWindow)
     return fail(W2V_ERR_UNSUPPORTED, "window must be in [0, 127]");
-  if (cfg->negative < 0 || cfg->negative > 63)
+  if (cfg->negative < 0 || cfg->negative > kMaxNegative)
     return fail(W2V_ERR_UNSUPPORTED, "negative must be in [0, 63]");
   if (!cfg->hs && cfg->negative == 0)
     return fail(W2V_ERR_ARG, "neither hs nor negative sampling enabled");

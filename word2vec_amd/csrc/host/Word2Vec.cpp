@@ -194,6 +194,7 @@ void Word2Vec::file_samples(const std::string& path, const std::string& format, 
 }
 
 void Word2Vec::train_file(const std::string& path, const std::string& format, int threads) {
+  check_limits();
   std::vector<int32_t> ids;
   std::vector<int64_t> offsets;
   int64_t train_words = 0;
@@ -614,8 +615,23 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
   release();
 }
 
+// The reference accepts any window / negative / word_dim (Word2Vec.cpp:254,
+// 285, 335); the kernels have a range (w2v_dev_limits). Checked before any
+// corpus work, naming the member.
+void Word2Vec::check_limits() const {
+  int32_t md = 0, mw = 0, mn = 0, smw = 0, smn = 0;
+  (void)w2v_dev_limits(&md, &mw, &mn, &smw, &smn);
+  auto bad = [](const std::string& what) { throw std::invalid_argument("word2vec_amd: " + what); };
+  if (word_dim < 1 || word_dim > md) bad("word_dim must be in [1, " + std::to_string(md) + "] on the GPU path");
+  if (window < 0 || window > mw) bad("window must be in [0, " + std::to_string(mw) + "] on the GPU path");
+  if (negative < 0 || negative > mn) bad("negative must be in [0, " + std::to_string(mn) + "] on the GPU path");
+  if (shared_negatives && (window > smw || negative > smn))
+    bad("shared_negatives needs window <= " + std::to_string(smw) + " and negative <= " + std::to_string(smn));
+}
+
 // Word2Vec.cpp:356-396.
 void Word2Vec::train(std::vector<std::vector<std::string>>& sentences) {
+  check_limits();
   if (!resume_) init_weights(vocab.size());
   int64_t train_words = 0;
   for (auto& s : sentences) train_words += (int64_t)s.size();
@@ -633,6 +649,7 @@ void Word2Vec::train(std::vector<std::vector<std::string>>& sentences) {
 
 void Word2Vec::train_ids(const std::vector<int32_t>& ids, const std::vector<int64_t>& offsets,
                          int64_t train_words) {
+  check_limits();
   if (!resume_) init_weights(vocab.size());
   run_epochs(ids, offsets, train_words);
 }

@@ -123,6 +123,27 @@ int main(int argc, char** argv) {
     std::cout << "Please use negative sampling in aligned skip gram model!" << std::endl;
     return 1;
   }
+  {  // the GPU kernels' range (w2v_dev_limits); the reference accepts any value
+    int32_t md = 0, mw = 0, mn = 0, smw = 0, smn = 0;
+    w2v_dev_limits(&md, &mw, &mn, &smw, &smn);
+    if (word_dim < 1 || word_dim > md) {
+      std::cout << "Please set -size in [1, " << md << "] (the GPU kernels' range)!" << std::endl;
+      return 1;
+    }
+    if (window < 0 || window > mw) {
+      std::cout << "Please set -window in [0, " << mw << "] (the GPU kernels' range)!" << std::endl;
+      return 1;
+    }
+    if (negative > mn) {
+      std::cout << "Please set -negative <= " << mn << " (the GPU kernels' range)!" << std::endl;
+      return 1;
+    }
+    if (shared && (window > smw || negative > smn)) {
+      std::cout << "Please set -window <= " << smw << " and -negative <= " << smn << " with -shared-negatives 1!"
+                << std::endl;
+      return 1;
+    }
+  }
   if (cbow_mean) init_alpha = 0.05f;
 
   Word2Vec w2v(iter, window, min_count, table_size, word_dim, negative, subsample_threshold, init_alpha,
