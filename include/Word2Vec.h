@@ -162,6 +162,9 @@ class Word2Vec {
   void load_checkpoint(const std::string& path);
   int64_t current_words() const { return cur_words_; }
   int64_t epochs_done() const { return epochs_done_; }
+  // Wall seconds of each epoch of the last train call (the device epoch,
+  // w2v_dev_train_epoch / the replicas' rounds; no host setup or transfers).
+  std::vector<double> epoch_seconds;
   // Last device error (empty if none).
   std::string last_error;
 

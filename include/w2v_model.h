@@ -89,6 +89,8 @@ int w2v_model_load_checkpoint(w2v_model* m, const char* path);
  * "%d" = the epochs done); epochs of the last train call's schedule done. */
 int w2v_model_set_checkpoint_path(w2v_model* m, const char* path);
 int64_t w2v_model_epochs_done(w2v_model* m);
+/* Word2Vec::epoch_seconds[i] of the last train call (-1 when i is out of range). */
+double w2v_model_epoch_seconds(w2v_model* m, int64_t i);
 int64_t w2v_model_current_words(w2v_model* m);
 int w2v_model_read_vocab(w2v_model* m, const char* path);
 

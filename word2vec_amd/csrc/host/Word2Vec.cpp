@@ -7,6 +7,7 @@
 #include "Word2Vec.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -458,6 +459,7 @@ void Word2Vec::run_epochs(const std::vector<int32_t>& ids, const std::vector<int
   key_ = key;
   epochs_done_ = first;
   resume_ = false;
+  epoch_seconds.clear();
   for (int it = 0; it < iter; ++it) {
     if (!replay_rng) {
       std::shuffle(sample_idx.begin(), sample_idx.end(), generator);
@@ -466,7 +468,9 @@ void Word2Vec::run_epochs(const std::vector<int32_t>& ids, const std::vector<int
     if (it < first) continue;  // done before the checkpoint
     w2v_dev_stats st;
     std::memset(&st, 0, sizeof(st));
+    const auto t0 = std::chrono::steady_clock::now();
     check(w2v_dev_train_epoch(dev_, it, orders[(size_t)it].data(), &st), "w2v_dev_train_epoch");
+    epoch_seconds.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     int64_t cw = 0;
     check(w2v_dev_get_progress(dev_, &cw), "w2v_dev_get_progress");
     epochs_done_ = it + 1;
@@ -556,9 +560,11 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
     int64_t global = cont ? start_words_ : 0;  // the reference's current_words over all replicas (:359, :393)
     epochs_done_ = first;
     resume_ = false;
+    epoch_seconds.clear();
     for (int it = 0; it < iter; ++it) {
       std::shuffle(sample_idx.begin(), sample_idx.end(), generator);  // :373
       if (it < first) continue;  // done before the checkpoint
+      const auto t0 = std::chrono::steady_clock::now();
       // shards and their per-sentence word counts
       std::vector<std::vector<int64_t>> shard(R), cum(R);
       int64_t largest = 0;
@@ -583,6 +589,7 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
         global += words;
       }
       check(w2v_group_finish(grp), "w2v_group_finish");
+      epoch_seconds.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
       for (size_t i = 0; i < R; ++i) {
         w2v_dev_stats st;
         check(w2v_dev_read_stats(reps[i], &st), "w2v_dev_read_stats");

@@ -264,6 +264,9 @@ int w2v_model_set_checkpoint_path(w2v_model* m, const char* path) {
   return guard(m, [&] { m->w.checkpoint_path = path ? path : ""; });
 }
 int64_t w2v_model_epochs_done(w2v_model* m) { return m->w.epochs_done(); }
+double w2v_model_epoch_seconds(w2v_model* m, int64_t i) {
+  return (i >= 0 && i < (int64_t)m->w.epoch_seconds.size()) ? m->w.epoch_seconds[(size_t)i] : -1.0;
+}
 int w2v_model_save_vocab(w2v_model* m, const char* path) {
   return guard(m, [&] { m->w.save_vocab(path); });
 }

@@ -63,6 +63,7 @@ def _load():
             "w2v_model_load_checkpoint": (C.c_int, [P, S]),
             "w2v_model_set_checkpoint_path": (C.c_int, [P, S]),
             "w2v_model_epochs_done": (I64, [P]),
+            "w2v_model_epoch_seconds": (C.c_double, [P, I64]),
             "w2v_model_current_words": (I64, [P]),
             "w2v_model_read_vocab": (C.c_int, [P, S]),
         }
@@ -203,6 +204,14 @@ class Word2Vec:
     @property
     def epochs_done(self) -> int:
         return self.L.w2v_model_epochs_done(self.h)
+
+    @property
+    def epoch_seconds(self) -> list:
+        """Wall seconds of each device epoch of the last train call."""
+        out = []
+        while (t := self.L.w2v_model_epoch_seconds(self.h, len(out))) >= 0:
+            out.append(t)
+        return out
 
     @property
     def current_words(self) -> int:
