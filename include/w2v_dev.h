@@ -241,8 +241,12 @@ int w2v_dev_flush_policy(w2v_dev* h, int32_t* flush_centers, int32_t* context_fl
 int w2v_dev_set_private_rows(w2v_dev* h, int32_t n);
 /* With private_rows = -1: privatise only the rows (Huffman nodes for HS, and
  * CBOW context rows) a center updates at least `mu` times on average, from
- * the corpus statistics (0 = no rate limit: as many as fit, <= 64). */
+ * the corpus statistics (0 = no rate limit: as many as fit, <= 64; -1, the
+ * default = 0.1 for a launch with fewer sentences than the chip holds waves,
+ * else no limit). */
 int w2v_dev_set_private_rate(w2v_dev* h, float mu);
+/* The rate limit the last parallel launch used (0 = none). Additive. */
+int w2v_dev_private_rate_used(w2v_dev* h, float* mu);
 /* flush_centers: workgroup centers between flushes (0 = auto: 1024 for NS, 64
  * for HS); average_over: the concurrency a private row's summed deltas are
  * scaled down to (default 8; 0 = plain sum). */

@@ -24,7 +24,7 @@ PAIRED_SEEDS = {"planted": (1, 2, 3), "text8_like": (1, 2, 3), "text8_small": (1
 PAIRED_MODES = {"planted": ("sg_ns", "sg_hs", "cbow_ns", "cbow_hs"), "text8_like": ("sg_ns", "cbow_hs"),
                 "text8_small": ("sg_ns", "cbow_hs")}
 ONE_WAVE_CORPORA = ("planted", "text8_small")
-FULL_CORPORA = ("planted", "text8_like")
+FULL_CORPORA = ("planted", "text8_like", "text8_small")
 
 
 def corpus(name):

@@ -63,7 +63,7 @@ def _compare(o, d, order, tol, elem_tol, tag):
 def test_shared_single_sentence(dim):
     sents = zipf_sentences(1, 160, 80, seed=21)
     o, d = _setup(sents, dim)
-    st = _compare(o, d, np.arange(1), 1e-5, 1e-3, f"shared single d{dim}")
+    st = _compare(o, d, np.arange(1), 1e-5, 5e-3, f"shared single d{dim}")
     assert st["centers"] > 0 and st["targets"] > st["centers"]
     d.close()
 
@@ -73,7 +73,7 @@ def test_shared_epoch(window, negative):
     sents = zipf_sentences(12, 200, 300, seed=23, ragged=True)
     o, d = _setup(sents, 128, window=window, negative=negative)
     n = o.samples()[1].size - 1
-    _compare(o, d, np.random.default_rng(1).permutation(n), 1e-4, 1e-2, f"shared epoch w{window} neg{negative}")
+    _compare(o, d, np.random.default_rng(1).permutation(n), 1e-4, 5e-3, f"shared epoch w{window} neg{negative}")
     d.close()
 
 

@@ -167,10 +167,12 @@ struct w2v_dev {
   std::vector<double> f, fk, node_f, node_fk;
   double hot_tau_rows = 0.0;        // automatic hot rows: expected concurrent updates threshold, W / C rows (0 = by vocab, hot_tau_for)
   double hot_tau_nodes = 1.0;       //   ... and Huffman nodes
-  double private_rate = 0.0;        // > 0: privatise only rows updated >= this many times per center (private_by_rate)
+  double private_rate = -1.0;       // > 0: privatise only rows updated >= this many times per center (private_by_rate);
+                                    // 0: no rate limit; < 0 (default): kSmallLaunchRate for a launch smaller than the chip
   // the policy the last parallel launch used (w2v_dev_policy)
   int64_t last_hot_rows = 0, last_hot_nodes = 0;
   double last_tau_rows = 0.0;
+  double last_private_rate = 0.0;
   int32_t last_priv = 0, last_ctx = 0;
   int32_t last_flush = 0, last_ctx_flush = 0;
 };
@@ -870,6 +872,27 @@ static std::pair<int64_t, int64_t> private_by_rate(w2v_dev* h, double mu) {
   return {out, ctx};
 }
 
+// The private-row rate limit a launch of `count` sentences uses (private_rate
+// < 0, the default): kSmallLaunchRate when the launch has fewer sentences than
+// the chip holds waves, else none. Such a launch (a small corpus, a replica's
+// round slice) puts every sentence on its own wave for the whole launch, so
+// every frequent row is held by thousands of waves at once and the LDS rows'
+// averaged flush damps rows that do not need it: text8_small (2 M tokens,
+// 2,000 sentences for 8,192 waves) CBOW-HS at full concurrency scored -9.5 /
+// -18.8 against the sequential oracle with no limit and +24.4 / +18.9 at 0.1;
+// SG-NS +5.3 / -0.2 and +6.1 / +5.2; the planted corpus (3,000 sentences) holds
+// every gate (+10.8 / +4.8, +1.1 / +0.3, +9.7 / +0.3, +19.8 / +2.5 over the four
+// modes; profiles/r03b_small_corpus.log). A launch that fills the chip keeps
+// no limit: there the limit costs 20 % of throughput.
+constexpr double kSmallLaunchRate = 0.1;
+static double private_rate_for(const w2v_dev* h, int64_t count) {
+  if (h->private_rate >= 0.0) return h->private_rate;
+  const int64_t per_simd = h->nv <= 2 ? 8 : 4;  // kMinWaves<NV>
+  int64_t chip = (int64_t)h->n_cu * 4 * per_simd;
+  if (h->max_waves > 0) chip = std::min(chip, h->max_waves);
+  return count < chip ? kSmallLaunchRate : 0.0;
+}
+
 // Automatic hot rows (hot_rows == W2V_HOT_AUTO): the rows (and Huffman nodes)
 // whose expected number of updates in flight across the chip, waves x their
 // expected updates per center, is at least hot_tau. A row that several
@@ -1093,8 +1116,10 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     const int64_t avail = hs ? h->V - 1 : h->V;
     if (P > avail) P = avail;
     std::pair<int64_t, int64_t> by_rate{P, w2v::kCtxMax};
-    if (h->private_rate > 0.0) {
-      by_rate = private_by_rate(h, h->private_rate);
+    const double rate = private_rate_for(h, count);
+    h->last_private_rate = rate;
+    if (rate > 0.0) {
+      by_rate = private_by_rate(h, rate);
       if (h->private_rows < 0) P = std::min(P, by_rate.first);
     }
     if (P > 0) {
@@ -1109,7 +1134,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     int64_t Q = h->cfg.cbow ? std::min<int64_t>({fit - P, (int64_t)w2v::kCtxMax, h->V}) : 0;
     if (h->context_rows < 0 && !h->cfg.hs) Q = 0;
     if (h->context_rows >= 0) Q = std::min<int64_t>(Q, h->context_rows);
-    else if (h->private_rate > 0.0) Q = std::min(Q, by_rate.second);
+    else if (rate > 0.0) Q = std::min(Q, by_rate.second);
     if (Q > 0) {
       a.ctx_M = h->C;
       a.ctx_n = (int32_t)Q;
@@ -1384,7 +1409,7 @@ int w2v_dev_set_hot_rows(w2v_dev* h, int64_t hot_rows) {
 
 int w2v_dev_set_private_rate(w2v_dev* h, float mu) {
   if (!h) return fail(W2V_ERR_ARG, "null handle");
-  if (!(mu >= 0.0f)) return fail(W2V_ERR_ARG, "private_rate must be >= 0");
+  if (!(mu >= 0.0f) && mu != -1.0f) return fail(W2V_ERR_ARG, "private_rate must be >= 0 (or -1: automatic)");
   h->private_rate = mu;
   return W2V_OK;
 }
@@ -1411,6 +1436,12 @@ int w2v_dev_hot_tau(w2v_dev* h, float* tau_rows, float* tau_nodes) {
   if (!h) return fail(W2V_ERR_ARG, "null handle");
   if (tau_rows) *tau_rows = (float)h->last_tau_rows;
   if (tau_nodes) *tau_nodes = (float)h->hot_tau_nodes;
+  return W2V_OK;
+}
+
+int w2v_dev_private_rate_used(w2v_dev* h, float* mu) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (mu) *mu = (float)h->last_private_rate;
   return W2V_OK;
 }
 

@@ -220,15 +220,19 @@ class DeviceTrainer:
         self._chk(self.lib.w2v_dev_flush_policy(self.h, C.byref(f), C.byref(cf)), "w2v_dev_flush_policy")
         tr, tn = C.c_float(), C.c_float()
         self._chk(self.lib.w2v_dev_hot_tau(self.h, C.byref(tr), C.byref(tn)), "w2v_dev_hot_tau")
+        mu = C.c_float()
+        self._chk(self.lib.w2v_dev_private_rate_used(self.h, C.byref(mu)), "w2v_dev_private_rate_used")
         return {"hot_rows": r.value, "hot_nodes": n.value, "private_rows": p.value, "context_rows": c.value,
-                "flush_centers": f.value, "context_flush": cf.value, "hot_tau_rows": tr.value}
+                "flush_centers": f.value, "context_flush": cf.value, "hot_tau_rows": tr.value,
+                "private_rate": round(mu.value, 4)}
 
     def set_private_rows(self, n: int):
         """Hottest output rows privatised per workgroup in LDS: -1 auto (default), 0 off."""
         self._chk(self.lib.w2v_dev_set_private_rows(self.h, int(n)), "w2v_dev_set_private_rows")
 
     def set_private_rate(self, mu: float):
-        """Privatise only rows updated >= mu times per center (0 = no rate limit)."""
+        """Privatise only rows updated >= mu times per center (0 = no rate limit, -1 = automatic: 0.1 for a
+        launch with fewer sentences than the chip holds waves)."""
         self._chk(self.lib.w2v_dev_set_private_rate(self.h, float(mu)), "w2v_dev_set_private_rate")
 
     def set_private_sync(self, flush_centers: int = 0, average_over: float = 8.0):
