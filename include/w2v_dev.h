@@ -336,6 +336,7 @@ int w2v_group_set_overlap(w2v_group* g, int32_t on);
 #define W2V_GROUP_SUM 0
 #define W2V_GROUP_AVERAGE 1
 #define W2V_GROUP_ROW_AVERAGE 2
+#define W2V_GROUP_ADAPTIVE 3 /* per row: the sum divided by max(1, |sum D|^2 / sum |D|^2) */
 int w2v_group_set_mode(w2v_group* g, int32_t mode);
 int w2v_group_average_async(w2v_group* g);
 int w2v_group_finish(w2v_group* g);

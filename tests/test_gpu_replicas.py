@@ -27,14 +27,17 @@ def _pair_of_handles(mode="sg_ns", dim=72):
     return o, [device_from_oracle(o, cfg, initial=False) for _ in range(2)]
 
 
-@pytest.mark.parametrize("gmode", ["row_average", "sum", "average"])
+@pytest.mark.parametrize("gmode", ["row_average", "sum", "average", "adaptive"])
 @pytest.mark.parametrize("overlap", [False, True])
 @pytest.mark.parametrize("mode", ["sg_ns", "cbow_hs"])
 def test_group_exchange(mode, overlap, gmode):
     """Both replicas start from M0 (the shared model P), then hold M1 and M2
     (M1 changes every row, M2 only the even rows): the exchange gives
-    M0 + (M1 - M0) + (M2 - M0) (sum), (M1 + M2) / 2 (average), or per row the
-    mean of the changes of the replicas that changed it (row_average)."""
+    M0 + (M1 - M0) + (M2 - M0) (sum), (M1 + M2) / 2 (average), per row the
+    mean of the changes of the replicas that changed it (row_average), or per
+    row the sum of the changes divided by max(1, |sum|^2 / sum of |change|^2)
+    (adaptive). Replica 1's changes of rows 0 mod 4 equal replica 0's (a row
+    both moved the same way: adaptive takes their mean there)."""
     o, ds = _pair_of_handles(mode)
     rng = np.random.default_rng(3)
     M0 = [None if m is None else rng.standard_normal(m.shape).astype(np.float32) for m in ds[0].download_model()]
@@ -53,6 +56,7 @@ def test_group_exchange(mode, overlap, gmode):
             dm = 0.1 * rng.standard_normal(m.shape)
             if i == 1:
                 dm[1::2] = 0.0  # replica 1 leaves the odd rows alone
+                dm[0::4] = (mats[0][len(Mi)] - m)[0::4]  # ... and moves rows 0 mod 4 as replica 0 did
             Mi.append((m + dm).astype(np.float32))
         d.upload_model(*Mi)
         mats.append(Mi)
@@ -66,6 +70,12 @@ def test_group_exchange(mode, overlap, gmode):
             want.append((a + b) / 2)
         elif gmode == "sum":
             want.append(a + b - z)
+        elif gmode == "adaptive":
+            da, db = (a - z).astype(np.float64), (b - z).astype(np.float64)
+            tot = da + db
+            den = (da * da).sum(1, keepdims=True) + (db * db).sum(1, keepdims=True)
+            c = np.where(den > 0, (tot * tot).sum(1, keepdims=True) / np.where(den > 0, den, 1), 1.0)
+            want.append(z + tot / np.maximum(1.0, c))
         else:
             cnt = 1.0 + (np.abs(b - z).max(1, keepdims=True) > 0)
             want.append(z + ((a - z) + (b - z)) / cnt)
@@ -78,7 +88,7 @@ def test_group_exchange(mode, overlap, gmode):
         d.close()
 
 
-@pytest.mark.parametrize("gmode", ["sum", "row_average", "average"])
+@pytest.mark.parametrize("gmode", ["sum", "row_average", "average", "adaptive"])
 @pytest.mark.parametrize("overlap", [False, True])
 def test_rccl_exchange_one_rank(overlap, gmode):
     """The RCCL exchange path on one GPU: a group built from a unique id with

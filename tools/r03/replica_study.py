@@ -178,14 +178,12 @@ def train(args, R, rounds, gmode, overlap, seed, data, dev):
             t.synchronize()
     dt = time.time() - t0
     Wf, Cf, _ = reps[0].download_model()
-    for t in reps:
-        st = t.read_stats()
-        assert st["nonfinite"] == 0
+    diverged = any(t.read_stats()["nonfinite"] > 0 for t in reps)
     if g is not None:
         g.close()
     for t in reps:
         t.close()
-    return (Cf if hs else Wf), dt
+    return (None if diverged else (Cf if hs else Wf)), dt
 
 
 def main():
@@ -200,26 +198,32 @@ def main():
     ap.add_argument("--gmodes", default="sum,average,row_average")
     ap.add_argument("--overlap", type=int, default=1)
     ap.add_argument("--seeds", default="1")
+    ap.add_argument("--planted-frac", type=float, default=0.10)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     t0 = time.time()
-    tok, n_sent, names, qs, prs = planted_zipf_ids(args.tokens, filler=args.filler, seed=0)
+    tok, n_sent, names, qs, prs = planted_zipf_ids(args.tokens, filler=args.filler, planted_frac=args.planted_frac,
+                                                   seed=0)
     args.raw_tokens = tok.size
     ids, soff, counts, words = build(tok, n_sent, 1000, names)
     del tok
     print(json.dumps({"corpus_tokens": int(args.raw_tokens), "in_vocab": int(ids.size), "V": int(counts.size),
                       "sentences": int(n_sent), "gen_s": round(time.time() - t0, 1), "mode": args.mode,
-                      "dim": args.dim, "iters": args.iters}), flush=True)
+                      "dim": args.dim, "iters": args.iters, "planted_frac": args.planted_frac}), flush=True)
     data = (ids, soff, counts, words, args.mode)
     for seed in [int(s) for s in args.seeds.split(",")]:
         E, dt = train(args, 1, 1, "sum", False, seed, data, dev)
         a1, s1 = gpu_scores(words, E, qs, prs, dev)
         print(json.dumps({"seed": seed, "R": 1, "analogy": round(a1, 2), "similarity": round(s1, 2),
                           "train_s": round(dt, 2)}), flush=True)
-        for R in [int(x) for x in args.replicas.split(",")]:
-            for rounds in [int(x) for x in args.rounds.split(",")]:
+        for R in [int(x) for x in args.replicas.split(",") if x]:
+            for rounds in [int(x) for x in args.rounds.split(",") if x]:
                 for gm in args.gmodes.split(","):
                     E, dt = train(args, R, rounds, gm, bool(args.overlap), seed, data, dev)
+                    if E is None:
+                        print(json.dumps({"seed": seed, "R": R, "rounds_per_epoch": rounds, "gmode": gm,
+                                          "overlap": bool(args.overlap), "diverged": True}), flush=True)
+                        continue
                     a, s = gpu_scores(words, E, qs, prs, dev)
                     print(json.dumps({"seed": seed, "R": R, "rounds_per_epoch": rounds, "gmode": gm,
                                       "overlap": bool(args.overlap), "analogy": round(a, 2),

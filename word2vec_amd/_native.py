@@ -25,6 +25,7 @@ W2V_GROUP_ID_BYTES = 128
 W2V_GROUP_SUM = 0
 W2V_GROUP_AVERAGE = 1
 W2V_GROUP_ROW_AVERAGE = 2
+W2V_GROUP_ADAPTIVE = 3
 W2V_RNG_PHILOX = 0
 W2V_RNG_REPLAY = 1
 W2V_SCHED_PARALLEL = 0

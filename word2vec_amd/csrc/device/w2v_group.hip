@@ -10,7 +10,12 @@
 //                             the shared model then, identical on every replica)
 //   A   = sum_i D_i          (one ncclAllReduce per matrix over xGMI)
 //   M_i <- P + A / c, P <- M_i
-// with c per row. W2V_GROUP_SUM (default): c = 1 — every update counts once,
+// with c per row. W2V_GROUP_ADAPTIVE: c = the row's coherence |sum D|^2 /
+// sum |D|^2 (at least 1): the mean of the replicas' moves of a row they all
+// moved the same way (a frequent row each replica drives to the same optimum:
+// summing R such moves overshoots R-fold and diverges), the sum of
+// independent moves (a rare row each replica saw a different part of).
+// W2V_GROUP_SUM: c = 1 — every update counts once,
 // as in the reference's one shared model; the replicas are Hogwild threads
 // whose writes become visible to each other at the round boundary.
 // W2V_GROUP_ROW_AVERAGE: c = the number of replicas whose round changed the
@@ -130,6 +135,46 @@ __global__ void row_touch_kernel(const float* D, int64_t pitch, int64_t rows, fl
   }
 }
 
+// One wavefront per row: sum of squares of the row's pitch floats (float4
+// loads across the lanes, shuffle reduction).
+__device__ __forceinline__ float row_sumsq(const float* row, int64_t pitch) {
+  const int lane = (int)(threadIdx.x & 63);
+  const float4* q = reinterpret_cast<const float4*>(row);
+  float acc = 0.f;
+  for (int64_t j = lane; j < pitch / 4; j += 64) {
+    const float4 v = q[j];
+    acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  return acc;
+}
+
+// F[r] = |row r of D|^2 (this replica's update of the row this round).
+__global__ void row_norm2_kernel(const float* D, int64_t pitch, int64_t rows, float* F) {
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / 64);
+  for (int64_t r = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; r < rows; r += waves) {
+    const float ss = row_sumsq(D + r * pitch, pitch);
+    if ((threadIdx.x & 63) == 0) F[r] = ss;
+  }
+}
+
+// W2V_GROUP_ADAPTIVE: FA[r] (the sum over replicas of |D_i,r|^2) becomes the
+// row's coherence c = |A_r|^2 / FA[r] in [0, R] (A = sum of the D_i): c = R
+// when the replicas moved the row identically, 1 when their moves were
+// orthogonal. The fold divides the row's summed update by max(1, c)
+// (row_weight): the mean where the replicas agree, the sum where they are
+// independent.
+__global__ void row_coherence_kernel(const float* A, int64_t pitch, int64_t rows, float* FA) {
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / 64);
+  for (int64_t r = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; r < rows; r += waves) {
+    const float ss = row_sumsq(A + r * pitch, pitch);
+    if ((threadIdx.x & 63) == 0) {
+      const float den = FA[r];
+      FA[r] = den > 0.f ? ss / den : 1.0f;
+    }
+  }
+}
+
 }  // namespace w2v
 
 namespace {
@@ -167,7 +212,8 @@ struct w2v_group {
   int64_t elems[3] = {0, 0, 0};  // floats per matrix (rows x pitch), 0 = unused
   int64_t rounds = 0;       // exchanges issued
   float scale() const { return mode == W2V_GROUP_AVERAGE ? 1.0f / (float)nranks : 1.0f; }
-  bool rows_counted() const { return mode == W2V_GROUP_ROW_AVERAGE; }
+  bool rows_counted() const { return mode == W2V_GROUP_ROW_AVERAGE || mode == W2V_GROUP_ADAPTIVE; }
+  bool adaptive() const { return mode == W2V_GROUP_ADAPTIVE; }
   int64_t rows(int k) const { return pitch > 0 ? elems[k] / pitch : 0; }
 };
 
@@ -251,6 +297,11 @@ int sum_deltas(w2v_group* g, bool on_comm) {
                              (g->rows(k) + 3) & ~int64_t(3));
           HIP_G(hipGetLastError());
         }
+        if (g->adaptive()) {
+          hipLaunchKernelGGL(w2v::row_coherence_kernel, dim3(kGrid), dim3(kBlock), 0, s0, x0.A[k], g->pitch,
+                             g->rows(k), x0.FA[k]);
+          HIP_G(hipGetLastError());
+        }
       }
     HIP_G(hipEventRecord(x0.done, s0));
     return W2V_OK;
@@ -278,7 +329,15 @@ int sum_deltas(w2v_group* g, bool on_comm) {
   NCCL_G(ncclGroupEnd());
   for (auto& x : g->m) {
     HIP_G(hipSetDevice(x.device));
-    HIP_G(hipEventRecord(x.done, on_comm ? x.comm : x.train));
+    hipStream_t st = on_comm ? x.comm : x.train;
+    if (g->adaptive())
+      for (int k = 0; k < 3; ++k)
+        if (g->elems[k]) {
+          hipLaunchKernelGGL(w2v::row_coherence_kernel, dim3(kGrid), dim3(kBlock), 0, st, x.A[k], g->pitch, g->rows(k),
+                             x.FA[k]);
+          HIP_G(hipGetLastError());
+        }
+    HIP_G(hipEventRecord(x.done, st));
   }
   return W2V_OK;
 }
@@ -410,7 +469,8 @@ int w2v_group_set_overlap(w2v_group* g, int32_t on) {
 
 int w2v_group_set_mode(w2v_group* g, int32_t mode) {
   if (!g) return fail_g(W2V_ERR_ARG, "null group");
-  if (mode != W2V_GROUP_SUM && mode != W2V_GROUP_AVERAGE && mode != W2V_GROUP_ROW_AVERAGE)
+  if (mode != W2V_GROUP_SUM && mode != W2V_GROUP_AVERAGE && mode != W2V_GROUP_ROW_AVERAGE &&
+      mode != W2V_GROUP_ADAPTIVE)
     return fail_g(W2V_ERR_ARG, "bad group mode");
   if (g->pending) return fail_g(W2V_ERR_STATE, "w2v_group_set_mode: an exchange is in flight (w2v_group_finish first)");
   g->mode = mode;
@@ -439,7 +499,11 @@ int w2v_group_average_async(w2v_group* g) {
                            fold ? sum_of(g, i, k) : nullptr, fold ? count_of(g, i, k) : nullptr, g->scale(),
                            fold ? 1 : 0, g->pitch, g->elems[k]);
         HIP_G(hipGetLastError());
-        if (g->rows_counted()) {
+        if (g->adaptive()) {
+          hipLaunchKernelGGL(w2v::row_norm2_kernel, dim3(kGrid), dim3(kBlock), 0, x.train, x.D[k], g->pitch, g->rows(k),
+                             x.F[k]);
+          HIP_G(hipGetLastError());
+        } else if (g->rows_counted()) {
           hipLaunchKernelGGL(w2v::row_touch_kernel, dim3(kGrid), dim3(kBlock), 0, x.train, x.D[k], g->pitch, g->rows(k),
                              x.F[k]);
           HIP_G(hipGetLastError());

@@ -114,7 +114,8 @@ class NativeAverager:
         self.g = g
         self.trainers = trainers
         N.check(self.lib, self.lib.w2v_group_set_overlap(self.g, int(bool(overlap))), "w2v_group_set_overlap")
-        modes = {"row_average": N.W2V_GROUP_ROW_AVERAGE, "sum": N.W2V_GROUP_SUM, "average": N.W2V_GROUP_AVERAGE}
+        modes = {"row_average": N.W2V_GROUP_ROW_AVERAGE, "sum": N.W2V_GROUP_SUM, "average": N.W2V_GROUP_AVERAGE,
+                 "adaptive": N.W2V_GROUP_ADAPTIVE}
         N.check(self.lib, self.lib.w2v_group_set_mode(self.g, modes[mode]), "w2v_group_set_mode")
 
     def average(self) -> None:
