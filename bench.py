@@ -194,7 +194,7 @@ def main():
     torch.cuda.set_stream(stream)
     tr.set_stream(stream.cuda_stream)
     tr.upload_vocab(keep, bounds, codes, points, coff)
-    pitch = (d + 63) // 64 * 64
+    pitch = tr.row_pitch()  # the kernels' row width (64 x floats per lane), zero padding
     vrows = V
     gW = torch.Generator(device=dev)
     gW.manual_seed(args.seed)  # identical initial replicas on every rank

@@ -15,7 +15,8 @@
  * handle's HIP stream (w2v_dev_set_stream).
  *
  * Device layout (HBM): W, C and synapses1 are row-major fp32 with a row pitch
- * of round_up(word_dim, 64) floats (256-B aligned rows; a per-pair kernel lane
+ * of w2v_dev_row_pitch floats (64 x the instantiated floats per lane covering
+ * word_dim: 256-B aligned rows, zero padding; a per-pair kernel lane
  * owns elements lane + 64 v of a row, the shared-negatives kernel's wave w of
  * n the columns [pitch/n w, pitch/n (w+1))); the unigram table is
  * uint32[table_size]; sample probabilities fp32[V]; Huffman paths are CSR
@@ -138,9 +139,15 @@ int w2v_dev_upload_rows(w2v_dev* h, int32_t which, const int32_t* rows, int64_t 
 int w2v_dev_download_rows(w2v_dev* h, int32_t which, const int32_t* rows, int64_t n, float* data);
 /* Train on caller-owned device matrices instead (e.g. torch tensors that an
  * RCCL all-reduce also touches): rows of `pitch` floats (pitch % 4 == 0,
- * pitch >= word_dim, 16-B aligned bases), padding columns zero. NULL for a
- * matrix the configuration does not use. The handle never frees them. */
+ * pitch >= w2v_dev_row_pitch, 16-B aligned bases), padding columns zero
+ * (the kernels read and write whole rows of w2v_dev_row_pitch floats and keep
+ * the padding zero). NULL for a matrix the configuration does not use. The
+ * handle never frees them. */
 int w2v_dev_bind_model(w2v_dev* h, float* dW, float* dC, float* dsyn1, int64_t pitch);
+/* The smallest row pitch (floats) the kernels accept: 64 x the instantiated
+ * floats per lane covering word_dim (d 300 -> 320, d 700 -> 768). The
+ * library-owned matrices use it. */
+int w2v_dev_row_pitch(w2v_dev* h, int64_t* pitch);
 /* Device pointers and row pitch (floats) of the resident matrices, for
  * collectives (RCCL model averaging) on the caller's side. */
 int w2v_dev_model_layout(w2v_dev* h, float** dW, float** dC, float** dsyn1, int64_t* pitch);
@@ -337,7 +344,13 @@ int w2v_group_set_overlap(w2v_group* g, int32_t on);
 #define W2V_GROUP_AVERAGE 1
 #define W2V_GROUP_ROW_AVERAGE 2
 #define W2V_GROUP_ADAPTIVE 3 /* per row: the sum divided by max(1, |sum D|^2 / sum |D|^2) */
+#define W2V_GROUP_SPLIT 4    /* per row: the mean for rows saturated within a round, else the sum */
 int w2v_group_set_mode(w2v_group* g, int32_t mode);
+/* W2V_GROUP_SPLIT: rows a replica is expected to update >= saturated_updates
+ * times in a round of tokens_per_round raw tokens (the corpus statistics of
+ * member 0) take the mean of the replicas' updates, the rest their sum. */
+int w2v_group_set_split(w2v_group* g, int64_t tokens_per_round, float saturated_updates);
+int w2v_group_split_rows(w2v_group* g, int64_t* rows); /* rows averaged (all matrices) */
 int w2v_group_average_async(w2v_group* g);
 int w2v_group_finish(w2v_group* g);
 int w2v_group_info(w2v_group* g, int32_t* nranks, int32_t* local, int32_t* overlap, int64_t* rounds);

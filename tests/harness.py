@@ -86,9 +86,15 @@ def errs(a, b):
 def check_parity(got, want, init, norm_tol, elem_tol, tag=""):
     """Assert both bounds on every matrix's update (got - init vs want - init):
     norm-wise rel_err < norm_tol AND per-element elem_rel_err < elem_tol; a
-    matrix the oracle left untouched must come back bit-identical. Each
-    measurement is printed and, with W2V_PARITY_LOG=<file>, appended to it as
-    a JSON line (the measured errors the bounds in the tests come from)."""
+    matrix the oracle left untouched must come back bit-identical. A matrix
+    whose update is far below its values (CBOW-NS's W in a single sentence:
+    C starts at zero, so W moves by ~1e-6 of its magnitude) is instead held to
+    the fp32 rounding of its stored values: max |got - want| <= 2 ulp of max
+    |want| (one rounding of `row + g * x` differing in the last bit, from a g
+    that differs in the 7th digit, is 1 ulp of the row, which relative to such
+    an update exceeds 1e-5). Each measurement is printed and, with
+    W2V_PARITY_LOG=<file>, appended to it as a JSON line (the measured errors
+    the bounds in the tests come from)."""
     import json
     import os
 
@@ -101,14 +107,16 @@ def check_parity(got, want, init, norm_tol, elem_tol, tag=""):
             np.testing.assert_array_equal(g, w)
             continue
         en, ee = errs(np.asarray(g, np.float64) - i, dw)
-        out.append((k, en, ee))
-        print(f"{tag} matrix {k}: rel_err {en:.2e} elem_rel_err {ee:.2e}")
+        abs_err = float(np.abs(np.asarray(g, np.float64) - np.asarray(w, np.float64)).max())
+        ulps = abs_err / float(np.spacing(np.float32(np.abs(w).max())))
+        out.append((k, en, ee, ulps))
+        print(f"{tag} matrix {k}: rel_err {en:.2e} elem_rel_err {ee:.2e} max_abs_err {ulps:.2f} ulp")
         path = os.environ.get("W2V_PARITY_LOG")
         if path:
             with open(path, "a") as f:
-                f.write(json.dumps({"tag": tag, "matrix": k, "rel_err": en, "elem_rel_err": ee,
+                f.write(json.dumps({"tag": tag, "matrix": k, "rel_err": en, "elem_rel_err": ee, "ulps": ulps,
                                     "norm_tol": norm_tol, "elem_tol": elem_tol}) + "\n")
-    for k, en, ee in out:
-        assert en < norm_tol, (tag, k, en, norm_tol)
+    for k, en, ee, ulps in out:
+        assert en < norm_tol or ulps <= 2.0, (tag, k, en, norm_tol, ulps)
         assert ee < elem_tol, (tag, k, ee, elem_tol)
     return out

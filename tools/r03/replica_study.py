@@ -149,7 +149,13 @@ def train(args, R, rounds, gmode, overlap, seed, data, dev):
         t.set_rng(N.W2V_RNG_PHILOX, (seed << 32) | 0x5EED)
         t.set_schedule(N.W2V_SCHED_PARALLEL)
         reps.append(t)
-    g = NativeAverager(reps, overlap=overlap, mode=gmode) if R > 1 else None
+    g = None
+    if R > 1:
+        if gmode.startswith("split"):  # split<n*>: mean for rows saturated within a round (>= n* updates)
+            g = NativeAverager(reps, overlap=overlap, mode="sum")
+            g.split_rows = g.set_split(max(1, int(args.raw_tokens) // R // rounds), float(gmode[5:]))
+        else:
+            g = NativeAverager(reps, overlap=overlap, mode=gmode)
     lens = np.diff(soff)
     glob = 0
     t0 = time.time()

@@ -26,6 +26,7 @@ W2V_GROUP_SUM = 0
 W2V_GROUP_AVERAGE = 1
 W2V_GROUP_ROW_AVERAGE = 2
 W2V_GROUP_ADAPTIVE = 3
+W2V_GROUP_SPLIT = 4
 W2V_RNG_PHILOX = 0
 W2V_RNG_REPLAY = 1
 W2V_SCHED_PARALLEL = 0
@@ -91,6 +92,7 @@ SIGNATURES = {
     "w2v_dev_upload_rows": (C.c_int, [_P, _I32, _P, _I64, _P]),
     "w2v_dev_download_rows": (C.c_int, [_P, _I32, _P, _I64, _P]),
     "w2v_dev_bind_model": (C.c_int, [_P, _P, _P, _P, _I64]),
+    "w2v_dev_row_pitch": (C.c_int, [_P, C.POINTER(_I64)]),
     "w2v_dev_model_layout": (C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), C.POINTER(_I64)]),
     "w2v_dev_upload_corpus": (C.c_int, [_P, _P, _I64, _P, _I64, _I64]),
     "w2v_dev_upload_replay": (C.c_int, [_P, _P, _I64, _P, _I64]),
@@ -125,6 +127,8 @@ SIGNATURES = {
     "w2v_group_destroy": (None, [_P]),
     "w2v_group_set_overlap": (C.c_int, [_P, _I32]),
     "w2v_group_set_mode": (C.c_int, [_P, _I32]),
+    "w2v_group_set_split": (C.c_int, [_P, _I64, _F]),
+    "w2v_group_split_rows": (C.c_int, [_P, C.POINTER(_I64)]),
     "w2v_group_average_async": (C.c_int, [_P]),
     "w2v_group_finish": (C.c_int, [_P]),
     "w2v_group_info": (C.c_int, [_P, C.POINTER(_I32), C.POINTER(_I32), C.POINTER(_I32), C.POINTER(_I64)]),

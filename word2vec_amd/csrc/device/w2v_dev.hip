@@ -223,6 +223,43 @@ static void row_stats(w2v_dev* h) {
   }
 }
 
+namespace w2v {
+// Per kept center (Word2Vec.cpp:319-353 SG, :273-317 CBOW): skip-gram updates
+// the center's W row once, the C row of every context (win1 = window + 1 on
+// average over the shrunk windows) and of neg table draws per context, and
+// the Huffman nodes of every context's path; CBOW the C rows of the contexts,
+// the W row of the center and of neg draws, and the center's path. Times the
+// kept fraction of the tokens.
+bool row_update_rates(w2v_dev* h, int k, std::vector<double>& out) {
+  row_stats(h);
+  const int64_t V = h->V;
+  out.clear();
+  if (!h->stats_ok || h->tok_count.empty()) return false;
+  double N = 0.0;
+  for (int64_t c : h->tok_count) N += (double)c;
+  const double q = N > 0.0 ? h->kept_tokens / N : 0.0;
+  const double win1 = (double)h->cfg.window + 1.0, neg = (double)h->cfg.negative;
+  const bool cbow = h->cfg.cbow != 0;
+  auto u = [&](int64_t r) { return r < (int64_t)h->table_frac.size() ? h->table_frac[(size_t)r] : 0.0; };
+  if (k == 2) {
+    if ((int64_t)h->node_f.size() != V - 1) return false;
+    out.resize((size_t)(V - 1));
+    for (int64_t j = 0; j < V - 1; ++j)
+      out[(size_t)j] = q * (cbow ? h->node_fk[(size_t)j] : win1 * h->node_f[(size_t)j]);
+    return true;
+  }
+  out.resize((size_t)V);
+  for (int64_t r = 0; r < V; ++r) {
+    const double f = h->f[(size_t)r], fk = h->fk[(size_t)r];
+    double m;
+    if (k == 0) m = cbow ? (neg > 0 ? fk + neg * u(r) : 0.0) : fk;
+    else m = cbow ? win1 * f : win1 * (f + neg * u(r));
+    out[(size_t)r] = q * m;
+  }
+  return true;
+}
+}  // namespace w2v
+
 namespace {
 
 using KernelFn = w2v::KernelFn;
@@ -335,8 +372,8 @@ int w2v_dev_create(const w2v_dev_config* cfg, w2v_dev** out) {
   h->own_stream = true;
   h->n_cu = ncu > 0 ? ncu : 256;
   h->d4 = (cfg->word_dim + 3) & ~3;
-  h->pitch = (cfg->word_dim + 63) & ~63;
   h->nv = pick_nv(cfg->word_dim);
+  h->pitch = (int64_t)h->nv * w2v::kWave;  // the kernels' row width (w2v_kernels.hpp, Row I/O)
   h->need_C = cfg->negative > 0 || cfg->cbow;
   h->need_S = cfg->hs != 0;
   *out = h;
@@ -450,7 +487,7 @@ int w2v_dev_upload_vocab(w2v_dev* h, int64_t V, const float* keep, const int64_t
     if (!h->model_bound) { dfree(h->W); dfree(h->C); dfree(h->S); }
     h->W = h->C = h->S = nullptr;
     h->model_bound = false;
-    h->pitch = (h->cfg.word_dim + 63) & ~63;
+    h->pitch = (int64_t)h->nv * w2v::kWave;
     h->model_ready = false;
     h->tok_count.clear();  // the corpus statistics refer to the old ids
   }
@@ -622,7 +659,9 @@ int w2v_dev_download_rows(w2v_dev* h, int32_t which, const int32_t* rows, int64_
 int w2v_dev_bind_model(w2v_dev* h, float* dW, float* dC, float* dS, int64_t pitch) {
   if (!h || !dW) return fail(W2V_ERR_ARG, "w2v_dev_bind_model: null argument");
   if (h->V < 1) return fail(W2V_ERR_STATE, "upload the vocab before binding the model");
-  if (pitch < h->d4 || pitch % 4 != 0) return fail(W2V_ERR_ARG, "pitch must be >= word_dim rounded to 4 and a multiple of 4");
+  if (pitch < (int64_t)h->nv * w2v::kWave || pitch % 4 != 0)
+    return fail(W2V_ERR_ARG, std::string("pitch must be a multiple of 4 and >= w2v_dev_row_pitch (the kernels' row "
+                                         "width, ") + std::to_string((int64_t)h->nv * w2v::kWave) + " floats here)");
   if (h->need_C && !dC) return fail(W2V_ERR_ARG, "this configuration needs C");
   if (h->need_S && !dS) return fail(W2V_ERR_ARG, "this configuration needs synapses1");
   for (const float* p : {dW, dC, dS})
@@ -634,6 +673,12 @@ int w2v_dev_bind_model(w2v_dev* h, float* dW, float* dC, float* dS, int64_t pitc
   h->pitch = pitch;
   h->model_bound = true;
   h->model_ready = true;
+  return W2V_OK;
+}
+
+int w2v_dev_row_pitch(w2v_dev* h, int64_t* pitch) {
+  if (!h || !pitch) return fail(W2V_ERR_ARG, "null argument");
+  *pitch = (int64_t)h->nv * w2v::kWave;
   return W2V_OK;
 }
 

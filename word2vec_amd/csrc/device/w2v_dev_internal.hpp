@@ -6,6 +6,7 @@
 
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "w2v_dev.h"
 #include "w2v_ingest.h"
@@ -21,6 +22,11 @@ struct DevInfo {
   int64_t V;
 };
 DevInfo dev_info(const w2v_dev* h);
+
+// Expected updates of each row of matrix k (0 = W, 1 = C, 2 = synapses1) per
+// corpus token, from the corpus statistics the handle holds (the rates the
+// update policy uses); false when the statistics are missing.
+bool row_update_rates(w2v_dev* h, int k, std::vector<double>& out);
 
 // The device samples of a mapped ingest (w2v_ingest.hip) for w2v_dev_adopt_corpus.
 struct IngestView {

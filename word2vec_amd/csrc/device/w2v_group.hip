@@ -15,6 +15,11 @@
 // moved the same way (a frequent row each replica drives to the same optimum:
 // summing R such moves overshoots R-fold and diverges), the sum of
 // independent moves (a rare row each replica saw a different part of).
+// W2V_GROUP_SPLIT: c = R for the rows a replica is expected to update at
+// least `saturated_updates` times per round (from the corpus statistics: such
+// a row reaches its local optimum within the round in every replica, and the
+// sum of R such moves overshoots R-fold), c = 1 for the rest (small,
+// independent moves that one model would have made one after another).
 // W2V_GROUP_SUM: c = 1 — every update counts once,
 // as in the reference's one shared model; the replicas are Hogwild threads
 // whose writes become visible to each other at the round boundary.
@@ -195,6 +200,7 @@ struct Member {
   float* A[3] = {nullptr, nullptr, nullptr};    // sum over replicas of D (same device: replica 0's only)
   float* F[3] = {nullptr, nullptr, nullptr};    // rows this replica changed (ROW_AVERAGE)
   float* FA[3] = {nullptr, nullptr, nullptr};   // contributors per row, summed (same device: replica 0's only)
+  float* WC[3] = {nullptr, nullptr, nullptr};   // W2V_GROUP_SPLIT: per-row divisor (1 or nranks)
 };
 
 }  // namespace
@@ -211,6 +217,7 @@ struct w2v_group {
   bool pending = false;     // an overlapped exchange is in flight
   int64_t elems[3] = {0, 0, 0};  // floats per matrix (rows x pitch), 0 = unused
   int64_t rounds = 0;       // exchanges issued
+  int64_t split_rows = 0;   // W2V_GROUP_SPLIT: rows (all matrices) averaged instead of summed
   float scale() const { return mode == W2V_GROUP_AVERAGE ? 1.0f / (float)nranks : 1.0f; }
   bool rows_counted() const { return mode == W2V_GROUP_ROW_AVERAGE || mode == W2V_GROUP_ADAPTIVE; }
   bool adaptive() const { return mode == W2V_GROUP_ADAPTIVE; }
@@ -237,7 +244,7 @@ void free_member(Member& x) {
   if (x.comm) (void)hipStreamSynchronize(x.comm);
   if (x.train) (void)hipStreamSynchronize(x.train);
   for (int k = 0; k < 3; ++k) {
-    for (float** b : {&x.P[k], &x.D[k], &x.A[k], &x.F[k], &x.FA[k]}) {
+    for (float** b : {&x.P[k], &x.D[k], &x.A[k], &x.F[k], &x.FA[k], &x.WC[k]}) {
       if (*b) (void)hipFree(*b);
       *b = nullptr;
     }
@@ -253,6 +260,7 @@ void free_member(Member& x) {
 
 const float* sum_of(const w2v_group* g, size_t i, int k) { return g->local ? g->m[0].A[k] : g->m[i].A[k]; }
 const float* count_of(const w2v_group* g, size_t i, int k) {
+  if (g->mode == W2V_GROUP_SPLIT) return g->m[i].WC[k];
   if (!g->rows_counted()) return nullptr;
   return g->local ? g->m[0].FA[k] : g->m[i].FA[k];
 }
@@ -471,9 +479,43 @@ int w2v_group_set_mode(w2v_group* g, int32_t mode) {
   if (!g) return fail_g(W2V_ERR_ARG, "null group");
   if (mode != W2V_GROUP_SUM && mode != W2V_GROUP_AVERAGE && mode != W2V_GROUP_ROW_AVERAGE &&
       mode != W2V_GROUP_ADAPTIVE)
-    return fail_g(W2V_ERR_ARG, "bad group mode");
+    return fail_g(W2V_ERR_ARG, "bad group mode (W2V_GROUP_SPLIT is set by w2v_group_set_split)");
   if (g->pending) return fail_g(W2V_ERR_STATE, "w2v_group_set_mode: an exchange is in flight (w2v_group_finish first)");
   g->mode = mode;
+  return W2V_OK;
+}
+
+int w2v_group_set_split(w2v_group* g, int64_t tokens_per_round, float saturated_updates) {
+  w2v::Range range_("w2v_group_set_split");
+  if (!g) return fail_g(W2V_ERR_ARG, "null group");
+  if (tokens_per_round < 1 || !(saturated_updates > 0.0f))
+    return fail_g(W2V_ERR_ARG, "w2v_group_set_split: tokens_per_round >= 1 and saturated_updates > 0");
+  if (g->pending) return fail_g(W2V_ERR_STATE, "w2v_group_set_split: an exchange is in flight (w2v_group_finish first)");
+  // the per-row divisors from member 0's corpus statistics (every replica
+  // trains the same vocabulary on a shard of the same corpus)
+  std::vector<float> wc[3];
+  for (int k = 0; k < 3; ++k) {
+    if (!g->elems[k]) continue;
+    std::vector<double> rate;
+    if (!w2v::row_update_rates(g->m[0].h, k, rate) || (int64_t)rate.size() != g->rows(k))
+      return fail_g(W2V_ERR_STATE, "w2v_group_set_split: the replicas need their vocab and corpus statistics uploaded");
+    wc[k].resize(rate.size());
+    for (size_t r = 0; r < rate.size(); ++r)
+      wc[k][r] = rate[r] * (double)tokens_per_round >= (double)saturated_updates ? (float)g->nranks : 1.0f;
+  }
+  for (auto& x : g->m) {
+    HIP_G(hipSetDevice(x.device));
+    for (int k = 0; k < 3; ++k) {
+      if (!g->elems[k]) continue;
+      if (!x.WC[k]) HIP_G(hipMalloc(&x.WC[k], wc[k].size() * sizeof(float)));
+      HIP_G(hipMemcpy(x.WC[k], wc[k].data(), wc[k].size() * sizeof(float), hipMemcpyHostToDevice));
+    }
+  }
+  int64_t avg = 0;
+  for (int k = 0; k < 3; ++k)
+    for (float w : wc[k]) avg += w > 1.0f;
+  g->split_rows = avg;
+  g->mode = W2V_GROUP_SPLIT;
   return W2V_OK;
 }
 
@@ -527,6 +569,12 @@ int w2v_group_finish(w2v_group* g) {
     HIP_G(hipStreamSynchronize(x.train));
     HIP_G(hipStreamSynchronize(x.comm));
   }
+  return W2V_OK;
+}
+
+int w2v_group_split_rows(w2v_group* g, int64_t* rows) {
+  if (!g || !rows) return fail_g(W2V_ERR_ARG, "null argument");
+  *rows = g->mode == W2V_GROUP_SPLIT ? g->split_rows : 0;
   return W2V_OK;
 }
 

@@ -263,21 +263,33 @@ __device__ __forceinline__ PrivRows ctx_rows(const TrainArgs& a, float* lds) {
 }
 
 // ---------------------------------------------------------------------------
-// Row I/O: a row is NV floats per lane, element lane + 64 v (v < NV).
+// Row I/O: a row is NV floats per lane, element lane + 64 v (v < NV). Rows
+// are NV * 64 floats apart at least (pitch >= NV * 64, w2v_dev_bind_model)
+// and their columns past word_dim are zero, and stay zero: every delta there
+// is g * 0. So every lane loads, stores and adds its whole row, with no
+// per-element guard: no exec-mask branches around the memory instructions
+// (an exec-masked zero-fill of a register whose load may be outstanding made
+// the compiler wait for ALL this wave's memory operations — vmcnt(0), stores
+// and memory-side atomics included — before every hot row's gather), and
+// every store writes whole 128-B lines. The dot products add the padding's
+// zeros, so the sums are bit-identical to the guarded form.
 // ---------------------------------------------------------------------------
+#ifndef W2V_ROW_GUARDS  // timing experiments only (tools/r03): 1 = the per-element guards of round 2
+#define W2V_ROW_GUARDS 0
+#endif
 template <int NV>
-__device__ __forceinline__ void load_row(const float* M, int64_t row, int64_t pitch, int d, int lane,
-                                         bool fresh, float (&r)[NV]) {
+__device__ __forceinline__ void load_row(const float* M, int64_t row, int64_t pitch, int d, int lane, bool fresh,
+                                         float (&r)[NV]) {
   const float* p = M + row * pitch + lane;
   if (fresh) {  // agent-scope relaxed loads: global_load_dword sc1, bypass the CU's L1
 #pragma unroll
     for (int v = 0; v < NV; ++v)
-      r[v] = (lane + kWave * v < d)
+      r[v] = (!W2V_ROW_GUARDS || lane + kWave * v < d)
                  ? __hip_atomic_load(p + kWave * v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                  : 0.f;
   } else {
 #pragma unroll
-    for (int v = 0; v < NV; ++v) r[v] = (lane + kWave * v < d) ? p[kWave * v] : 0.f;
+    for (int v = 0; v < NV; ++v) r[v] = (!W2V_ROW_GUARDS || lane + kWave * v < d) ? p[kWave * v] : 0.f;
   }
 }
 
@@ -287,10 +299,14 @@ __device__ __forceinline__ void store_row(float* M, int64_t row, int64_t pitch, 
   float* p = M + row * pitch + lane;
 #pragma unroll
   for (int v = 0; v < NV; ++v)
-    if (lane + kWave * v < d) p[kWave * v] = r[v];
+    if (!W2V_ROW_GUARDS || lane + kWave * v < d) p[kWave * v] = r[v];
 }
 
-// row += delta, memory-side (no-return global_atomic_add_f32, 256 contiguous B per instruction)
+// row += delta, memory-side (no-return global_atomic_add_f32, 256 contiguous B
+// per instruction). The padding lanes are masked here: an atomic has no
+// destination register (nothing to zero-fill, no wait), and a memory-side add
+// of 0 would still cost the atomic unit a request (d 300: 320 adds per row
+// instead of 300; measured 2.5 % of configs[2], profiles/r03d_guards_ab.log).
 template <int NV>
 __device__ __forceinline__ void atomic_add_row(float* M, int64_t row, int64_t pitch, int d, int lane,
                                                const float (&delta)[NV]) {
@@ -442,11 +458,9 @@ __device__ __forceinline__ void flush_private(const TrainArgs& a, const PrivRows
     float* dst = pr.M + (pr.lo + p) * a.pitch + lane;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      if (lane + kWave * v < a.dim) {
-        const float val = atomicExch(q + kWave * v, 0.0f);
-        if (val != 0.0f && !(W2V_EXP_SKIP & 2))
-          (void)__hip_atomic_fetch_add(dst + kWave * v, val * sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      const float val = atomicExch(q + kWave * v, 0.0f);  // 0 past word_dim: skipped
+      if (val != 0.0f && !(W2V_EXP_SKIP & 2))
+        (void)__hip_atomic_fetch_add(dst + kWave * v, val * sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -537,7 +551,11 @@ __device__ __forceinline__ void hs_apply(const TrainArgs& a, int T, int row_l, i
 template <int NV, int MAXT>
 __device__ __forceinline__ void hs_word(const TrainArgs& a, int word, int lane, const float (&x)[NV],
                                         float (&g)[NV], float alpha, Counters& cnt, float* lds) {
+#ifndef W2V_HS_MT
   constexpr int MT = MAXT / 2 > 0 ? MAXT / 2 : 1;  // two buffers of MT rows: the same registers as one of MAXT
+#else  // experiments (tools/r03): rows per pipelined batch
+  constexpr int MT = W2V_HS_MT;
+#endif
   const PrivRows pr = (a.priv_M == a.S) ? out_rows<NV>(a, lds) : PrivRows();
   const int64_t cb = a.coff[word];
   const int L = (int)(a.coff[word + 1] - cb);

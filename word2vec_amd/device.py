@@ -118,6 +118,12 @@ class DeviceTrainer:
         self._chk(self.lib.w2v_dev_bind_model(self.h, C.c_void_p(dW), C.c_void_p(dC) if dC else None,
                                               C.c_void_p(dS) if dS else None, int(pitch)), "w2v_dev_bind_model")
 
+    def row_pitch(self) -> int:
+        """The smallest row pitch (floats) bind_model accepts: the kernels' row width."""
+        p = C.c_int64()
+        self._chk(self.lib.w2v_dev_row_pitch(self.h, C.byref(p)), "w2v_dev_row_pitch")
+        return p.value
+
     def model_layout(self):
         w, c, s, p = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_int64()
         self._chk(self.lib.w2v_dev_model_layout(self.h, C.byref(w), C.byref(c), C.byref(s), C.byref(p)),

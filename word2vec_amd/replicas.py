@@ -118,6 +118,16 @@ class NativeAverager:
                  "adaptive": N.W2V_GROUP_ADAPTIVE}
         N.check(self.lib, self.lib.w2v_group_set_mode(self.g, modes[mode]), "w2v_group_set_mode")
 
+    def set_split(self, tokens_per_round: int, saturated_updates: float) -> int:
+        """W2V_GROUP_SPLIT: the mean of the replicas' updates for rows expected to be updated >=
+        saturated_updates times per replica in a round of tokens_per_round tokens, the sum for the rest.
+        Returns the number of averaged rows."""
+        self.N.check(self.lib, self.lib.w2v_group_set_split(self.g, int(tokens_per_round), float(saturated_updates)),
+                     "w2v_group_set_split")
+        n = C.c_int64()
+        self.N.check(self.lib, self.lib.w2v_group_split_rows(self.g, C.byref(n)), "w2v_group_split_rows")
+        return n.value
+
     def average(self) -> None:
         self.N.check(self.lib, self.lib.w2v_group_average_async(self.g), "w2v_group_average_async")
 
