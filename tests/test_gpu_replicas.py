@@ -27,7 +27,7 @@ def _pair_of_handles(mode="sg_ns", dim=72):
     return o, [device_from_oracle(o, cfg, initial=False) for _ in range(2)]
 
 
-@pytest.mark.parametrize("gmode", ["row_average", "sum", "average", "adaptive"])
+@pytest.mark.parametrize("gmode", ["row_average", "sum", "average", "adaptive", "split_all", "split_none"])
 @pytest.mark.parametrize("overlap", [False, True])
 @pytest.mark.parametrize("mode", ["sg_ns", "cbow_hs"])
 def test_group_exchange(mode, overlap, gmode):
@@ -43,7 +43,11 @@ def test_group_exchange(mode, overlap, gmode):
     M0 = [None if m is None else rng.standard_normal(m.shape).astype(np.float32) for m in ds[0].download_model()]
     for d in ds:
         d.upload_model(*M0)
-    g = NativeAverager(ds, overlap=overlap, mode=gmode)
+    g = NativeAverager(ds, overlap=overlap, mode=gmode if not gmode.startswith("split") else "sum")
+    if gmode.startswith("split"):  # every row saturated (-> the mean) or none (-> the sum)
+        n_avg = g.set_split(1000, 1e-9 if gmode == "split_all" else 1e30)
+        rows = sum(m.shape[0] for m in M0 if m is not None)
+        assert n_avg == (rows if gmode == "split_all" else 0)
     info = g.info()
     assert info["local"] and info["nranks"] == 2 and info["overlap"] == overlap
     mats = []
@@ -66,9 +70,9 @@ def test_group_exchange(mode, overlap, gmode):
     for a, b, z in zip(*mats, M0):
         if a is None:
             want.append(None)
-        elif gmode == "average":
+        elif gmode in ("average", "split_all"):
             want.append((a + b) / 2)
-        elif gmode == "sum":
+        elif gmode in ("sum", "split_none"):
             want.append(a + b - z)
         elif gmode == "adaptive":
             da, db = (a - z).astype(np.float64), (b - z).astype(np.float64)
