@@ -352,6 +352,12 @@ int w2v_group_set_mode(w2v_group* g, int32_t mode);
 int w2v_group_set_split(w2v_group* g, int64_t tokens_per_round, float saturated_updates);
 int w2v_group_split_rows(w2v_group* g, int64_t* rows); /* rows averaged (all matrices) */
 int w2v_group_average_async(w2v_group* g);
+/* The same exchange over the hottest rows only: rows [0, rows) of W and C
+ * (the most frequent words) and the `rows` Huffman nodes nearest the root of
+ * synapses1 (rows == 0: all). The other rows keep their own updates until a
+ * later exchange covers them (their deltas stay relative to the last exchange
+ * that did), so frequent hot-row exchanges between full ones are exact. */
+int w2v_group_average_rows_async(w2v_group* g, int64_t rows);
 int w2v_group_finish(w2v_group* g);
 int w2v_group_info(w2v_group* g, int32_t* nranks, int32_t* local, int32_t* overlap, int64_t* rounds);
 

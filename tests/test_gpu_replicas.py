@@ -92,6 +92,49 @@ def test_group_exchange(mode, overlap, gmode):
         d.close()
 
 
+@pytest.mark.parametrize("overlap", [False, True])
+@pytest.mark.parametrize("mode", ["sg_ns", "cbow_hs"])
+def test_group_hot_rows_exchange(mode, overlap):
+    """average(rows=k) exchanges W / C rows [0, k) and the k Huffman nodes
+    nearest the root only: those rows take the sum of both replicas' changes,
+    the others keep each replica's own; a full exchange after it completes the
+    sum for every row (their deltas stayed relative to the shared model)."""
+    o, ds = _pair_of_handles(mode)
+    rng = np.random.default_rng(7)
+    M0 = [None if m is None else rng.standard_normal(m.shape).astype(np.float32) for m in ds[0].download_model()]
+    for d in ds:
+        d.upload_model(*M0)
+    g = NativeAverager(ds, overlap=overlap, mode="sum")
+    mats = []
+    for d in ds:
+        Mi = [None if m is None else (m + 0.1 * rng.standard_normal(m.shape)).astype(np.float32) for m in M0]
+        d.upload_model(*Mi)
+        mats.append(Mi)
+    k = 40
+    g.average(rows=k)
+    g.finish()
+    for i, d in enumerate(ds):
+        for j, (got, a, b, z) in enumerate(zip(d.download_model(), mats[0], mats[1], M0)):
+            if z is None:
+                continue
+            hot = np.zeros(z.shape[0], bool)
+            if j == 2:
+                hot[-k:] = True
+            else:
+                hot[:k] = True
+            np.testing.assert_allclose(got[hot], (a + b - z)[hot], rtol=1e-5, atol=1e-5)
+            np.testing.assert_array_equal(got[~hot], mats[i][j][~hot])
+    g.average()
+    g.finish()
+    for d in ds:
+        for got, a, b, z in zip(d.download_model(), mats[0], mats[1], M0):
+            if z is not None:
+                np.testing.assert_allclose(got, a + b - z, rtol=1e-5, atol=1e-5)
+    g.close()
+    for d in ds:
+        d.close()
+
+
 @pytest.mark.parametrize("gmode", ["sum", "row_average", "average", "adaptive"])
 @pytest.mark.parametrize("overlap", [False, True])
 def test_rccl_exchange_one_rank(overlap, gmode):

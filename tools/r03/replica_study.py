@@ -166,17 +166,21 @@ def train(args, R, rounds, gmode, overlap, seed, data, dev):
         for t, sh in zip(reps, shards):
             t.set_order(sh)
             cums.append(np.concatenate([[0], np.cumsum(lens[sh])]))
-        for r in range(rounds):
+        # `rounds` full exchanges per epoch; with --hot-rows K, hot-row exchanges
+        # (W / C rows [0, K), the nodes nearest the root) at --hot-rounds per epoch between them
+        sub = max(rounds, args.hot_rounds) if args.hot_rows > 0 else rounds
+        per_full = max(1, sub // rounds)
+        for r in range(sub):
             words_r = 0
             for t, sh, cu in zip(reps, shards, cums):
                 m = sh.size
-                lo, hi = m * r // rounds, m * (r + 1) // rounds
+                lo, hi = m * r // sub, m * (r + 1) // sub
                 t.set_progress_async(glob // R)
                 if hi > lo:
                     t.train_slice_async(ep, lo, hi - lo)
                 words_r += int(cu[hi] - cu[lo])
             if g is not None:
-                g.average()
+                g.average(0 if (r + 1) % per_full == 0 else args.hot_rows)
             glob += words_r
         if g is not None:
             g.finish()
@@ -205,6 +209,8 @@ def main():
     ap.add_argument("--overlap", type=int, default=1)
     ap.add_argument("--seeds", default="1")
     ap.add_argument("--planted-frac", type=float, default=0.10)
+    ap.add_argument("--hot-rows", type=int, default=0, help="hot rows exchanged between the full exchanges (0 = none)")
+    ap.add_argument("--hot-rounds", type=int, default=0, help="hot-row exchanges per epoch")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     t0 = time.time()
@@ -218,7 +224,10 @@ def main():
                       "dim": args.dim, "iters": args.iters, "planted_frac": args.planted_frac}), flush=True)
     data = (ids, soff, counts, words, args.mode)
     for seed in [int(s) for s in args.seeds.split(",")]:
+        hr = args.hot_rows
+        args.hot_rows = 0
         E, dt = train(args, 1, 1, "sum", False, seed, data, dev)
+        args.hot_rows = hr
         a1, s1 = gpu_scores(words, E, qs, prs, dev)
         print(json.dumps({"seed": seed, "R": 1, "analogy": round(a1, 2), "similarity": round(s1, 2),
                           "train_s": round(dt, 2)}), flush=True)
@@ -228,10 +237,12 @@ def main():
                     E, dt = train(args, R, rounds, gm, bool(args.overlap), seed, data, dev)
                     if E is None:
                         print(json.dumps({"seed": seed, "R": R, "rounds_per_epoch": rounds, "gmode": gm,
+                                          "hot_rows": args.hot_rows, "hot_rounds": args.hot_rounds,
                                           "overlap": bool(args.overlap), "diverged": True}), flush=True)
                         continue
                     a, s = gpu_scores(words, E, qs, prs, dev)
                     print(json.dumps({"seed": seed, "R": R, "rounds_per_epoch": rounds, "gmode": gm,
+                                      "hot_rows": args.hot_rows, "hot_rounds": args.hot_rounds,
                                       "overlap": bool(args.overlap), "analogy": round(a, 2),
                                       "similarity": round(s, 2), "d_analogy": round(a - a1, 2),
                                       "d_similarity": round(s - s1, 2), "train_s": round(dt, 2)}), flush=True)

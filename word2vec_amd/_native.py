@@ -130,6 +130,7 @@ SIGNATURES = {
     "w2v_group_set_split": (C.c_int, [_P, _I64, _F]),
     "w2v_group_split_rows": (C.c_int, [_P, C.POINTER(_I64)]),
     "w2v_group_average_async": (C.c_int, [_P]),
+    "w2v_group_average_rows_async": (C.c_int, [_P, _I64]),
     "w2v_group_finish": (C.c_int, [_P]),
     "w2v_group_info": (C.c_int, [_P, C.POINTER(_I32), C.POINTER(_I32), C.POINTER(_I32), C.POINTER(_I64)]),
     # include/w2v_ingest.h

@@ -80,6 +80,16 @@ __global__ void replica_sum_kernel(PtrList src, int n, float* out, int64_t n_ele
   }
 }
 
+// out = sum over n replicas' arrays, element-wise (scalar: per-row counts at any offset).
+__global__ void replica_sum1_kernel(PtrList src, int n, float* out, int64_t n_elems) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_elems; i += stride) {
+    float acc = src.p[0][i];
+    for (int k = 1; k < n; ++k) acc += src.p[k][i];
+    out[i] = acc;
+  }
+}
+
 // Per-row weight of the exchanged sum: 1 / max(1, contributors) (cnt) or s.
 __device__ __forceinline__ float row_weight(const float* cnt, float s, int64_t i4, int64_t pitch) {
   return cnt ? 1.0f / fmaxf(1.0f, cnt[(i4 * 4) / pitch]) : s;
@@ -222,6 +232,19 @@ struct w2v_group {
   bool rows_counted() const { return mode == W2V_GROUP_ROW_AVERAGE || mode == W2V_GROUP_ADAPTIVE; }
   bool adaptive() const { return mode == W2V_GROUP_ADAPTIVE; }
   int64_t rows(int k) const { return pitch > 0 ? elems[k] / pitch : 0; }
+  // Rows each exchange covers (w2v_group_average_rows_async): matrix k's rows
+  // [lo[k], lo[k] + n[k]); `cur` for the exchange being issued, `pend` for the
+  // one in flight (its deltas and sums live at the same offsets).
+  struct Span {
+    int64_t lo[3] = {0, 0, 0}, n[3] = {0, 0, 0};
+    bool operator==(const Span& o) const {
+      for (int k = 0; k < 3; ++k)
+        if (lo[k] != o.lo[k] || n[k] != o.n[k]) return false;
+      return true;
+    }
+  } cur, pend;
+  int64_t at(const Span& sp, int k) const { return sp.lo[k] * pitch; }    // element offset
+  int64_t len(const Span& sp, int k) const { return sp.n[k] * pitch; }   // elements
 };
 
 namespace {
@@ -258,11 +281,14 @@ void free_member(Member& x) {
   x.comm = nullptr;
 }
 
-const float* sum_of(const w2v_group* g, size_t i, int k) { return g->local ? g->m[0].A[k] : g->m[i].A[k]; }
-const float* count_of(const w2v_group* g, size_t i, int k) {
-  if (g->mode == W2V_GROUP_SPLIT) return g->m[i].WC[k];
+// The summed deltas / per-row divisors of replica i's matrix k over span sp.
+const float* sum_of(const w2v_group* g, size_t i, int k, const w2v_group::Span& sp) {
+  return (g->local ? g->m[0].A[k] : g->m[i].A[k]) + g->at(sp, k);
+}
+const float* count_of(const w2v_group* g, size_t i, int k, const w2v_group::Span& sp) {
+  if (g->mode == W2V_GROUP_SPLIT) return g->m[i].WC[k] + sp.lo[k];
   if (!g->rows_counted()) return nullptr;
-  return g->local ? g->m[0].FA[k] : g->m[i].FA[k];
+  return (g->local ? g->m[0].FA[k] : g->m[i].FA[k]) + sp.lo[k];
 }
 
 // Fold a finished exchange into every replica (train streams): M += s A - D, P = M.
@@ -272,10 +298,12 @@ int fold_pending(w2v_group* g) {
     Member& x = g->m[i];
     HIP_G(hipSetDevice(x.device));
     HIP_G(hipStreamWaitEvent(x.train, g->local ? g->m[0].done : x.done, 0));
+    const w2v_group::Span& sp = g->pend;
     for (int k = 0; k < 3; ++k)
-      if (g->elems[k]) {
-        hipLaunchKernelGGL(w2v::replica_fold_kernel, dim3(kGrid), dim3(kBlock), 0, x.train, x.mat[k], x.P[k], x.D[k],
-                           sum_of(g, i, k), count_of(g, i, k), g->scale(), g->pitch, g->elems[k]);
+      if (sp.n[k]) {
+        const int64_t o = g->at(sp, k);
+        hipLaunchKernelGGL(w2v::replica_fold_kernel, dim3(kGrid), dim3(kBlock), 0, x.train, x.mat[k] + o, x.P[k] + o,
+                           x.D[k] + o, sum_of(g, i, k, sp), count_of(g, i, k, sp), g->scale(), g->pitch, g->len(sp, k));
         HIP_G(hipGetLastError());
       }
   }
@@ -293,21 +321,24 @@ int sum_deltas(w2v_group* g, bool on_comm) {
     hipStream_t s0 = on_comm ? x0.comm : x0.train;
     HIP_G(hipSetDevice(x0.device));
     for (auto& x : g->m) HIP_G(hipStreamWaitEvent(s0, x.ready, 0));
+    const w2v_group::Span& sp = g->cur;
     for (int k = 0; k < 3; ++k)
-      if (g->elems[k]) {
+      if (sp.n[k]) {
+        const int64_t o = g->at(sp, k), lo = sp.lo[k];
         w2v::PtrList pl{};
-        for (size_t i = 0; i < n; ++i) pl.p[i] = g->m[i].D[k];
-        hipLaunchKernelGGL(w2v::replica_sum_kernel, dim3(kGrid), dim3(kBlock), 0, s0, pl, (int)n, x0.A[k], g->elems[k]);
+        for (size_t i = 0; i < n; ++i) pl.p[i] = g->m[i].D[k] + o;
+        hipLaunchKernelGGL(w2v::replica_sum_kernel, dim3(kGrid), dim3(kBlock), 0, s0, pl, (int)n, x0.A[k] + o,
+                           g->len(sp, k));
         HIP_G(hipGetLastError());
         if (g->rows_counted()) {
-          for (size_t i = 0; i < n; ++i) pl.p[i] = g->m[i].F[k];
-          hipLaunchKernelGGL(w2v::replica_sum_kernel, dim3(kGrid), dim3(kBlock), 0, s0, pl, (int)n, x0.FA[k],
-                             (g->rows(k) + 3) & ~int64_t(3));
+          for (size_t i = 0; i < n; ++i) pl.p[i] = g->m[i].F[k] + lo;
+          hipLaunchKernelGGL(w2v::replica_sum1_kernel, dim3(kGrid), dim3(kBlock), 0, s0, pl, (int)n, x0.FA[k] + lo,
+                             sp.n[k]);
           HIP_G(hipGetLastError());
         }
         if (g->adaptive()) {
-          hipLaunchKernelGGL(w2v::row_coherence_kernel, dim3(kGrid), dim3(kBlock), 0, s0, x0.A[k], g->pitch,
-                             g->rows(k), x0.FA[k]);
+          hipLaunchKernelGGL(w2v::row_coherence_kernel, dim3(kGrid), dim3(kBlock), 0, s0, x0.A[k] + o, g->pitch,
+                             sp.n[k], x0.FA[k] + lo);
           HIP_G(hipGetLastError());
         }
       }
@@ -319,15 +350,18 @@ int sum_deltas(w2v_group* g, bool on_comm) {
       HIP_G(hipSetDevice(x.device));
       HIP_G(hipStreamWaitEvent(x.comm, x.ready, 0));
     }
+  const w2v_group::Span& sp = g->cur;
   NCCL_G(ncclGroupStart());
   for (auto& x : g->m) {
     (void)hipSetDevice(x.device);
     for (int k = 0; k < 3; ++k)
-      if (g->elems[k]) {
-        ncclResult_t r = ncclAllReduce(x.D[k], x.A[k], (size_t)g->elems[k], ncclFloat32, ncclSum, x.nccl,
+      if (sp.n[k]) {
+        const int64_t o = g->at(sp, k), lo = sp.lo[k];
+        ncclResult_t r = ncclAllReduce(x.D[k] + o, x.A[k] + o, (size_t)g->len(sp, k), ncclFloat32, ncclSum, x.nccl,
                                        on_comm ? x.comm : x.train);
         if (r == ncclSuccess && g->rows_counted())
-          r = ncclAllReduce(x.F[k], x.FA[k], (size_t)g->rows(k), ncclFloat32, ncclSum, x.nccl, on_comm ? x.comm : x.train);
+          r = ncclAllReduce(x.F[k] + lo, x.FA[k] + lo, (size_t)sp.n[k], ncclFloat32, ncclSum, x.nccl,
+                            on_comm ? x.comm : x.train);
         if (r != ncclSuccess) {
           (void)ncclGroupEnd();
           return fail_g(W2V_ERR_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
@@ -340,13 +374,60 @@ int sum_deltas(w2v_group* g, bool on_comm) {
     hipStream_t st = on_comm ? x.comm : x.train;
     if (g->adaptive())
       for (int k = 0; k < 3; ++k)
-        if (g->elems[k]) {
-          hipLaunchKernelGGL(w2v::row_coherence_kernel, dim3(kGrid), dim3(kBlock), 0, st, x.A[k], g->pitch, g->rows(k),
-                             x.FA[k]);
+        if (sp.n[k]) {
+          hipLaunchKernelGGL(w2v::row_coherence_kernel, dim3(kGrid), dim3(kBlock), 0, st, x.A[k] + g->at(sp, k),
+                             g->pitch, sp.n[k], x.FA[k] + sp.lo[k]);
           HIP_G(hipGetLastError());
         }
     HIP_G(hipEventRecord(x.done, st));
   }
+  return W2V_OK;
+}
+
+// One exchange over g->cur (set by the callers below).
+int exchange(w2v_group* g) {
+  if (!g->exchange) return W2V_OK;
+  ++g->rounds;
+  // extract this round's deltas and fold the pending exchange in (overlap):
+  // fused into the delta kernel when the pending exchange covers the same
+  // rows, else folded first on its own rows
+  if (g->overlap && g->pending && !(g->pend == g->cur))
+    if (int rc = fold_pending(g)) return rc;
+  const bool fold = g->overlap && g->pending;
+  if (fold)
+    for (size_t i = 0; i < g->m.size(); ++i) {
+      Member& x = g->m[i];
+      HIP_G(hipSetDevice(x.device));
+      HIP_G(hipStreamWaitEvent(x.train, g->local ? g->m[0].done : x.done, 0));
+    }
+  const w2v_group::Span& sp = g->cur;
+  for (size_t i = 0; i < g->m.size(); ++i) {
+    Member& x = g->m[i];
+    HIP_G(hipSetDevice(x.device));
+    for (int k = 0; k < 3; ++k)
+      if (sp.n[k]) {
+        const int64_t o = g->at(sp, k), lo = sp.lo[k];
+        hipLaunchKernelGGL(w2v::replica_delta_kernel, dim3(kGrid), dim3(kBlock), 0, x.train, x.mat[k] + o, x.P[k] + o,
+                           x.D[k] + o, fold ? sum_of(g, i, k, sp) : nullptr, fold ? count_of(g, i, k, sp) : nullptr,
+                           g->scale(), fold ? 1 : 0, g->pitch, g->len(sp, k));
+        HIP_G(hipGetLastError());
+        if (g->adaptive()) {
+          hipLaunchKernelGGL(w2v::row_norm2_kernel, dim3(kGrid), dim3(kBlock), 0, x.train, x.D[k] + o, g->pitch,
+                             sp.n[k], x.F[k] + lo);
+          HIP_G(hipGetLastError());
+        } else if (g->rows_counted()) {
+          hipLaunchKernelGGL(w2v::row_touch_kernel, dim3(kGrid), dim3(kBlock), 0, x.train, x.D[k] + o, g->pitch,
+                             sp.n[k], x.F[k] + lo);
+          HIP_G(hipGetLastError());
+        }
+      }
+    HIP_G(hipEventRecord(x.ready, x.train));
+  }
+  g->pending = false;
+  if (int rc = sum_deltas(g, g->overlap)) return rc;
+  g->pending = true;
+  g->pend = g->cur;
+  if (!g->overlap) return fold_pending(g);  // blocking: fold in right away, on the training streams
   return W2V_OK;
 }
 
@@ -522,42 +603,23 @@ int w2v_group_set_split(w2v_group* g, int64_t tokens_per_round, float saturated_
 int w2v_group_average_async(w2v_group* g) {
   w2v::Range range_("w2v_group_average_async");
   if (!g) return fail_g(W2V_ERR_ARG, "null group");
-  if (!g->exchange) return W2V_OK;
-  ++g->rounds;
-  // extract this round's deltas (and fold the pending exchange in, overlap)
-  const bool fold = g->overlap && g->pending;
-  if (fold)
-    for (size_t i = 0; i < g->m.size(); ++i) {
-      Member& x = g->m[i];
-      HIP_G(hipSetDevice(x.device));
-      HIP_G(hipStreamWaitEvent(x.train, g->local ? g->m[0].done : x.done, 0));
-    }
-  for (size_t i = 0; i < g->m.size(); ++i) {
-    Member& x = g->m[i];
-    HIP_G(hipSetDevice(x.device));
-    for (int k = 0; k < 3; ++k)
-      if (g->elems[k]) {
-        hipLaunchKernelGGL(w2v::replica_delta_kernel, dim3(kGrid), dim3(kBlock), 0, x.train, x.mat[k], x.P[k], x.D[k],
-                           fold ? sum_of(g, i, k) : nullptr, fold ? count_of(g, i, k) : nullptr, g->scale(),
-                           fold ? 1 : 0, g->pitch, g->elems[k]);
-        HIP_G(hipGetLastError());
-        if (g->adaptive()) {
-          hipLaunchKernelGGL(w2v::row_norm2_kernel, dim3(kGrid), dim3(kBlock), 0, x.train, x.D[k], g->pitch, g->rows(k),
-                             x.F[k]);
-          HIP_G(hipGetLastError());
-        } else if (g->rows_counted()) {
-          hipLaunchKernelGGL(w2v::row_touch_kernel, dim3(kGrid), dim3(kBlock), 0, x.train, x.D[k], g->pitch, g->rows(k),
-                             x.F[k]);
-          HIP_G(hipGetLastError());
-        }
-      }
-    HIP_G(hipEventRecord(x.ready, x.train));
+  for (int k = 0; k < 3; ++k) {
+    g->cur.lo[k] = 0;
+    g->cur.n[k] = g->rows(k);
   }
-  g->pending = false;
-  if (int rc = sum_deltas(g, g->overlap)) return rc;
-  g->pending = true;
-  if (!g->overlap) return fold_pending(g);  // blocking: fold in right away, on the training streams
-  return W2V_OK;
+  return exchange(g);
+}
+
+int w2v_group_average_rows_async(w2v_group* g, int64_t rows) {
+  w2v::Range range_("w2v_group_average_rows_async");
+  if (!g) return fail_g(W2V_ERR_ARG, "null group");
+  if (rows < 0) return fail_g(W2V_ERR_ARG, "w2v_group_average_rows_async: rows must be >= 0");
+  for (int k = 0; k < 3; ++k) {  // W / C: the first rows (the most frequent words); synapses1: the nodes nearest the root
+    const int64_t R = g->rows(k), n = rows == 0 ? R : std::min(rows, R);
+    g->cur.lo[k] = k == 2 ? R - n : 0;
+    g->cur.n[k] = n;
+  }
+  return exchange(g);
 }
 
 int w2v_group_finish(w2v_group* g) {

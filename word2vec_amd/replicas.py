@@ -128,8 +128,14 @@ class NativeAverager:
         self.N.check(self.lib, self.lib.w2v_group_split_rows(self.g, C.byref(n)), "w2v_group_split_rows")
         return n.value
 
-    def average(self) -> None:
-        self.N.check(self.lib, self.lib.w2v_group_average_async(self.g), "w2v_group_average_async")
+    def average(self, rows: int = 0) -> None:
+        """Exchange all rows (rows == 0) or only the `rows` hottest (W / C rows [0, rows), the nodes nearest
+        the Huffman root)."""
+        if rows:
+            self.N.check(self.lib, self.lib.w2v_group_average_rows_async(self.g, int(rows)),
+                         "w2v_group_average_rows_async")
+        else:
+            self.N.check(self.lib, self.lib.w2v_group_average_async(self.g), "w2v_group_average_async")
 
     def finish(self) -> None:
         self.N.check(self.lib, self.lib.w2v_group_finish(self.g), "w2v_group_finish")
