@@ -12,3 +12,12 @@ for K in 4096 32768; do
   $S --rounds 8 --hot-rows $K --hot-rounds 512 --gmodes adaptive,sum,split1000,average > gpurun_out/$TAG/hot$K.log 2>&1 || exit 1
   grep -v amdgpu.ids gpurun_out/$TAG/hot$K.log | tail -4
 done
+# more LDS-private output rows on the SG-NS presets (fewer memory-side atomics)
+for c in c3 c1; do
+  for pr in -1 127; do
+    timeout -k 10 200 python bench.py --config $c --steps 3 --warmup 1 --cpu-seconds 0 --private-rows $pr > gpurun_out/$TAG/${c}_pr$pr.json 2> gpurun_out/$TAG/${c}_pr$pr.err || exit 1
+    echo "$c private_rows=$pr $(python -c "import json;d=json.load(open('gpurun_out/$TAG/${c}_pr$pr.json'));print(round(d['value']/1e6,2),d['roofline']['frac'],d['ms_per_step'],d['config']['policy_used'])")"
+  done
+done
+timeout -k 10 400 python -u tests/probes/quality_paired_probe.py text8_like sg_ns 1,2,3 0 "-;private_rows=127" > gpurun_out/$TAG/priv_quality.log 2>&1 || exit 1
+cat gpurun_out/$TAG/priv_quality.log
