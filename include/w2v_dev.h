@@ -348,7 +348,8 @@ int w2v_group_set_overlap(w2v_group* g, int32_t on);
 int w2v_group_set_mode(w2v_group* g, int32_t mode);
 /* W2V_GROUP_SPLIT: rows a replica is expected to update >= saturated_updates
  * times in a round of tokens_per_round raw tokens (the corpus statistics of
- * member 0) take the mean of the replicas' updates, the rest their sum. */
+ * member 0) take the mean of the replicas' updates, the rest their sum
+ * (saturated_updates 0: every row the mean). */
 int w2v_group_set_split(w2v_group* g, int64_t tokens_per_round, float saturated_updates);
 int w2v_group_split_rows(w2v_group* g, int64_t* rows); /* rows averaged (all matrices) */
 int w2v_group_average_async(w2v_group* g);

@@ -45,7 +45,7 @@ def test_group_exchange(mode, overlap, gmode):
         d.upload_model(*M0)
     g = NativeAverager(ds, overlap=overlap, mode=gmode if not gmode.startswith("split") else "sum")
     if gmode.startswith("split"):  # every row saturated (-> the mean) or none (-> the sum)
-        n_avg = g.set_split(1000, 1e-9 if gmode == "split_all" else 1e30)
+        n_avg = g.set_split(1000, 0.0 if gmode == "split_all" else 1e30)
         rows = sum(m.shape[0] for m in M0 if m is not None)
         assert n_avg == (rows if gmode == "split_all" else 0)
     info = g.info()

@@ -569,8 +569,8 @@ int w2v_group_set_mode(w2v_group* g, int32_t mode) {
 int w2v_group_set_split(w2v_group* g, int64_t tokens_per_round, float saturated_updates) {
   w2v::Range range_("w2v_group_set_split");
   if (!g) return fail_g(W2V_ERR_ARG, "null group");
-  if (tokens_per_round < 1 || !(saturated_updates > 0.0f))
-    return fail_g(W2V_ERR_ARG, "w2v_group_set_split: tokens_per_round >= 1 and saturated_updates > 0");
+  if (tokens_per_round < 1 || !(saturated_updates >= 0.0f))
+    return fail_g(W2V_ERR_ARG, "w2v_group_set_split: tokens_per_round >= 1 and saturated_updates >= 0");
   if (g->pending) return fail_g(W2V_ERR_STATE, "w2v_group_set_split: an exchange is in flight (w2v_group_finish first)");
   // the per-row divisors from member 0's corpus statistics (every replica
   // trains the same vocabulary on a shard of the same corpus)
