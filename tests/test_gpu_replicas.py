@@ -218,10 +218,10 @@ def _train_class(sents, mode, seed, gpu_devices, sync_words, overlap, max_waves)
     return words, w.matrix(1 if mode == "cbow_hs" else 0)
 
 
-# measured bound per mode (profiles/r02n_replicas64_*.log): CBOW-HS
-# lands within a point of one model; SG-NS loses ~4 (its summed negative-sample
-# updates of the frequent output rows overshoot)
-REPLICA_BOUND = {"cbow_hs": 1.0, "sg_ns": 5.0}
+# north_star's one point for both modes (round 2 allowed SG-NS 5 points; since
+# the round-3 small-launch policy, private_rate_for, two replicas score +2.2 /
+# +3.5 (SG-NS) and +1.0 / +0.4 (CBOW-HS) over one, profiles/r03c_gpu_tests.log)
+REPLICA_BOUND = {"cbow_hs": 1.0, "sg_ns": 1.0}
 
 
 @pytest.mark.parametrize("mode", ["sg_ns", "cbow_hs"])
