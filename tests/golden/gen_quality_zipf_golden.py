@@ -19,7 +19,8 @@ ZTRAIN = dict(dim=100, window=5, iters=1, table_size=100_000_000, min_count=5, s
 ZMODE = "sg_ns"
 ZSEEDS = (1, 2, 3)
 ZFILES = {"sg_ns": "quality_zipf_oracle.json", "cbow_hs": "quality_zipf_cbow_hs_oracle.json",
-          "sg_sn": "quality_zipf_sg_sn_oracle.json", "sg_ns_c5": "quality_zipf_sg_ns_c5_oracle.json"}
+          "sg_sn": "quality_zipf_sg_sn_oracle.json", "sg_ns_c5": "quality_zipf_sg_ns_c5_oracle.json",
+          "sg_sn_c5": "quality_zipf_sg_sn_c5_oracle.json"}
 # configs[4]'s hyper-parameters (BASELINE.json): d512, negative 15
 C5 = dict(dim=512, negative=15)
 
@@ -39,9 +40,20 @@ def one(seed, mode=ZMODE):
     from word2vec_amd.evaluate import analogy_accuracy, similarity_score
 
     sents, qs, pairs = planted_zipf_corpus(**ZCORPUS)
-    if mode == "sg_sn":  # configs[4]'s shared-negatives minibatch, sequential (oracle sgsn_sentence), neg 5
+    if mode in ("sg_sn", "sg_sn_c5"):  # the shared-negatives minibatch, sequential (oracle sgsn_sentence)
         import numpy as np
-        o = oracle_run(sents, "sg_ns", seed=seed, init_alpha=zalpha(mode), train=False, **ZTRAIN)
+        if mode == "sg_sn":  # neg 5 at ZTRAIN's d100
+            o = oracle_run(sents, "sg_ns", seed=seed, init_alpha=zalpha(mode), train=False, **ZTRAIN)
+        else:  # configs[4]'s d512 / negative 15
+            from oracle import Oracle
+            t = dict(ZTRAIN, dim=C5["dim"])
+            o = Oracle(iter=t["iters"], window=t["window"], min_count=t["min_count"], table_size=t["table_size"],
+                       word_dim=t["dim"], negative=C5["negative"], subsample_threshold=t["subsample"],
+                       init_alpha=zalpha(mode), min_alpha=2.5e-6, cbow_mean=True, train_method="ns", model="sg")
+            o.load_sentences(sents)
+            o.seed(seed)
+            o.build_vocab()
+            o.init_weights()
         o.build_sample()
         o.set_shared_negatives(True)
         order = np.random.default_rng(seed).permutation(len(sents)).astype(np.int64)
@@ -68,7 +80,7 @@ def one(seed, mode=ZMODE):
 def main(mode=ZMODE):
     with ProcessPoolExecutor(len(ZSEEDS)) as ex:
         res = list(ex.map(one, ZSEEDS, [mode] * len(ZSEEDS)))
-    train = dict(ZTRAIN, **C5) if mode == "sg_ns_c5" else ZTRAIN
+    train = dict(ZTRAIN, **C5) if mode in ("sg_ns_c5", "sg_sn_c5") else ZTRAIN
     out = {"corpus": ZCORPUS, "train": train, "mode": mode, "alpha": zalpha(mode), "scores": res}
     (ROOT / "tests" / "golden" / ZFILES[mode]).write_text(json.dumps(out, indent=1) + "\n")
     print(json.dumps(out, indent=1))
