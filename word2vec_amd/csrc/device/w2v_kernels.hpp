@@ -619,6 +619,106 @@ __device__ __forceinline__ void apply_list(const TrainArgs& a, float* M, int T, 
   cnt.targets += (unsigned long long)T;
 }
 
+// Two consecutive contexts' NS updates as one batch (skip-gram, negative <=
+// kPairNeg): context A's targets in slots [0, T1), context B's in [kPairHalf,
+// kPairHalf + T2). All rows are gathered at once, so B's gathers no longer
+// wait behind A's stores and memory-side atomics (vmcnt retires in order).
+// The reference applies A before B (Word2Vec.cpp:329-349): a B target that
+// is also one of A's takes A's updated row from the registers — the same fp32
+// `row + g * x` a re-read would return on the sequential schedule, so parity
+// is unchanged — and A's gradient terms accumulate before B's.
+constexpr int kPairHalf = 6;
+constexpr int kPairNeg = kPairHalf - 1;
+#ifndef W2V_NS_PAIR  // 0: one context per batch (experiments)
+#define W2V_NS_PAIR 1
+#endif
+template <int NV>
+constexpr bool kNsPair = W2V_NS_PAIR && NV >= 3;  // d <= 128 keeps 64 VGPRs (8 waves/SIMD): no room for 12 rows
+
+template <int NV>
+__device__ __forceinline__ void pair_update(float* M, int64_t pitch, int d, int lane, int row, bool hot, bool priv,
+                                            int code, float f, const float (&x)[NV], float (&g)[NV], float alpha,
+                                            float (&r)[NV], const PrivRows& pr, unsigned long long* stats) {
+  note_nonfinite(stats, !__builtin_isfinite(f), lane);
+  const float e = expf(-f);
+  const float s = (float)(1.0 / (double)(1.0f + e));
+  const float gt = ((float)(1 - code) - s) * alpha;
+  float delta[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    g[v] += gt * r[v];  // grad uses the pre-update row (:266)
+    delta[v] = gt * x[v];
+    r[v] += delta[v];   // the updated row, for a later target of the other context
+  }
+  if (priv) {
+    priv_add<NV>(pr, row, d, lane, delta);
+  } else if (hot) {
+    if (!(W2V_EXP_SKIP & 1)) atomic_add_row<NV>(M, row, pitch, d, lane, delta);
+  } else {
+    store_row<NV>(M, row, pitch, d, lane, r);
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void apply_pair(const TrainArgs& a, float* M, int T1, int T2, int row_l, int lane,
+                                           const float (&x)[NV], float (&g)[NV], float alpha, const PrivRows& pr) {
+  constexpr int H = kPairHalf, MP = 2 * kPairHalf;
+  float r[MP][NV];
+  int rows[MP];
+  bool hot[MP], priv[MP], use[MP];
+#pragma unroll
+  for (int t = 0; t < MP; ++t) {
+    use[t] = t < H ? t < T1 : t - H < T2;
+    rows[t] = readlane_i(row_l, t);
+    priv[t] = pr.has(rows[t]);
+    hot[t] = !priv[t] && rows[t] < a.hot_wc;
+    if (use[t]) load_row<NV>(M, rows[t], a.pitch, a.dim, lane, hot[t] || priv[t], r[t]);
+  }
+#pragma unroll
+  for (int t = 0; t < MP; ++t)
+    if (use[t] && priv[t]) priv_read<NV>(pr, rows[t], lane, r[t]);
+  // context A: every score from the gathered rows, then the updates in target order
+  float f[MP];
+#pragma unroll
+  for (int t = 0; t < H; ++t) {
+    f[t] = 0.f;
+    if (use[t]) {
+      float p = 0.f;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) p += r[t][v] * x[v];
+      f[t] = wave_sum(p);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < H; ++t)
+    if (use[t]) pair_update<NV>(M, a.pitch, a.dim, lane, rows[t], hot[t], priv[t], t == 0 ? 0 : 1, f[t], x, g, alpha,
+                                r[t], pr, a.stats);
+  // context B: a row A updated continues from A's result (targets of one
+  // context are distinct, so at most one A slot matches)
+#pragma unroll
+  for (int t = H; t < MP; ++t)
+#pragma unroll
+    for (int u = 0; u < H; ++u)
+      if (use[t] && use[u] && rows[t] == rows[u]) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) r[t][v] = r[u][v];
+      }
+#pragma unroll
+  for (int t = H; t < MP; ++t) {
+    f[t] = 0.f;
+    if (use[t]) {
+      float p = 0.f;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) p += r[t][v] * x[v];
+      f[t] = wave_sum(p);
+    }
+  }
+#pragma unroll
+  for (int t = H; t < MP; ++t)
+    if (use[t]) pair_update<NV>(M, a.pitch, a.dim, lane, rows[t], hot[t], priv[t], t == H ? 0 : 1, f[t], x, g, alpha,
+                                r[t], pr, a.stats);
+}
+
 // NS with positive `word` against `negw_l` lanes [base, base + neg).
 template <int NV, int MAXT>
 __device__ __forceinline__ void ns_word(const TrainArgs& a, float* M, int word, int negw_l, int base, int lane,
@@ -669,6 +769,33 @@ __device__ __forceinline__ void sg_center(const TrainArgs& a, float* lds, const 
   cnt.contexts += (unsigned long long)(span - 1);
   const int nctx = span - 1;
   const int neg = a.negative;
+  if (NS && !HS && kNsPair<NV> && neg <= kPairNeg && span <= kWave) {
+    // contexts two at a time (apply_pair); the table draws of G2 contexts at once
+    const int me = i - lo;
+    const int cw_l = sent[lo + min(lane + (lane >= me ? 1 : 0), span - 1)];  // lane k: the k-th context word
+    const int G2 = max(2, (kWave / neg) & ~1);
+    const PrivRows pr = (a.priv_M == a.C) ? out_rows<NV>(a, lds) : PrivRows();
+    int negw_l = 0;
+    for (int k = 0; k < nctx; k += 2) {
+      const int gs = k % G2;
+      if (gs == 0) {
+        const int nd = min(G2, nctx - k) * neg;
+        negw_l = draw_negatives<REPLAY>(a, s, (uint32_t)i, k, nd, lane, rp);
+        cnt.draws += (unsigned long long)nd;
+      }
+      int ta = 0, tb = 0;
+      const int T1 = ns_targets(neg, readlane_i(cw_l, k), negw_l, gs * neg, lane, ta);
+      const int T2 = (k + 1 < nctx) ? ns_targets(neg, readlane_i(cw_l, k + 1), negw_l, (gs + 1) * neg, lane, tb) : 0;
+      const int tgt_l = lane < kPairHalf ? ta : __shfl(tb, (lane - kPairHalf) & (kWave - 1));
+      if (a.strict) drain_vmem();
+      apply_pair<NV>(a, a.C, T1, T2, tgt_l, lane, x, g, alpha, pr);
+      cnt.targets += (unsigned long long)(T1 + T2);
+    }
+    cnt.stamp(3);
+    add_to_row<NV>(a.W, c, hot_c, a.pitch, a.dim, lane, g);  // W.row(center) += neu1_grad (:351)
+    cnt.stamp(4);
+    return;
+  }
   const int G = NS ? max(1, kWave / max(neg, 1)) : 1;
   int negw_l = 0;
   int slot = 0;
