@@ -245,6 +245,11 @@ int w2v_dev_policy(w2v_dev* h, int64_t* hot_rows, int64_t* hot_nodes, int32_t* p
  * >= 128 flushes per launch (context rows at half). Additive; no reference
  * counterpart. */
 int w2v_dev_flush_policy(w2v_dev* h, int32_t* flush_centers, int32_t* context_flush);
+/* Expected updates per raw corpus token of every row of matrix `which` (0 W,
+ * 1 C, 2 synapses1; n = its row count), from the uploaded vocab and corpus
+ * statistics: what the flush scales, the hot-row threshold and the replica
+ * exchange's per-row divisors are computed from. Additive. */
+int w2v_dev_row_update_rates(w2v_dev* h, int32_t which, double* out, int64_t n);
 int w2v_dev_set_private_rows(w2v_dev* h, int32_t n);
 /* With private_rows = -1: privatise only the rows (Huffman nodes for HS, and
  * CBOW context rows) a center updates at least `mu` times on average, from
@@ -345,13 +350,24 @@ int w2v_group_set_overlap(w2v_group* g, int32_t on);
 #define W2V_GROUP_ROW_AVERAGE 2
 #define W2V_GROUP_ADAPTIVE 3 /* per row: the sum divided by max(1, |sum D|^2 / sum |D|^2) */
 #define W2V_GROUP_SPLIT 4    /* per row: the mean for rows saturated within a round, else the sum */
+#define W2V_GROUP_SATURATION 5 /* per row: the sum divided by a smooth function of the row's updates per round */
 int w2v_group_set_mode(w2v_group* g, int32_t mode);
 /* W2V_GROUP_SPLIT: rows a replica is expected to update >= saturated_updates
  * times in a round of tokens_per_round raw tokens (the corpus statistics of
  * member 0) take the mean of the replicas' updates, the rest their sum
  * (saturated_updates 0: every row the mean). */
 int w2v_group_set_split(w2v_group* g, int64_t tokens_per_round, float saturated_updates);
-int w2v_group_split_rows(w2v_group* g, int64_t* rows); /* rows averaged (all matrices) */
+/* W2V_GROUP_SATURATION: the sum divided per row by
+ * c = R (1 - (1 - beta)^u) / (1 - (1 - beta)^(R u)), u = the row's expected
+ * updates per replica in a round of tokens_per_round raw tokens (member 0's
+ * corpus statistics) and beta the contraction of one update: what one model
+ * updating the row R u times in a row would move it (the sum for rarely
+ * updated rows, the mean for rows every replica saturates within the round). */
+int w2v_group_set_saturation(w2v_group* g, int64_t tokens_per_round, float beta);
+int w2v_group_split_rows(w2v_group* g, int64_t* rows); /* rows with a divisor > 1 (all matrices) */
+/* The per-row divisors W2V_GROUP_SPLIT / SATURATION apply to matrix `which`
+ * (n = its row count; all 1 in the other modes). */
+int w2v_group_row_divisors(w2v_group* g, int32_t which, float* out, int64_t n);
 int w2v_group_average_async(w2v_group* g);
 /* The same exchange over the hottest rows only: rows [0, rows) of W and C
  * (the most frequent words) and the `rows` Huffman nodes nearest the root of

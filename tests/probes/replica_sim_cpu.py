@@ -32,12 +32,32 @@ if warm > 0:  # replica 0 alone trains the first `warm` fraction, then the rest 
     order = order[nw:]
     n = len(order)
 shards = [order[n * i // R:n * (i + 1) // R] for i in range(R)]
+if how.startswith("sat"):  # sat<beta>: smooth saturation-corrected sum (w2v_group SATURATION)
+    from word2vec_amd import host as _host
+    _, cnt = o.vocab()
+    f = cnt / cnt.sum()
+    keep = np.minimum(1.0, _host.sample_probs(cnt, 1e-4).astype(np.float64))
+    fk = f * keep
+    qk = fk.sum()
+    u_tab = cnt ** 0.75 / (cnt ** 0.75).sum()
+    rate = {0: fk, 1: qk * 6.0 * (f + 5 * u_tab)}  # SG-NS per raw token (window 5: win1 = 6 on average... )
+    beta = float(how[3:])
+    tok_round = tw / R / rounds
+    WCS = {}
+    for k in mats:
+        u = rate[k] * tok_round
+        a = -np.expm1(u * np.log1p(-beta))
+        b = -np.expm1(R * u * np.log1p(-beta))
+        WCS[k] = np.where(b > 0, R * a / np.maximum(b, 1e-300), 1.0)
 for r in range(rounds):
     D = {k: np.zeros_like(P[k]) for k in mats}
     touched = {k: np.zeros(P[k].shape[0]) for k in mats}
+    sq = {k: np.zeros(P[k].shape[0]) for k in mats}
     for i in range(R):
         sh = shards[i]
         sl = sh[len(sh) * r // rounds: len(sh) * (r + 1) // rounds]
+        if len(sl) == 0:
+            continue
         # corpus = the slice's sentences (ids relabelled 0..m-1)
         sub_ids = np.concatenate([ids[off[s]:off[s + 1]] for s in sl])
         sub_off = np.concatenate([[0], np.cumsum([off[s + 1] - off[s] for s in sl])])
@@ -48,9 +68,14 @@ for r in range(rounds):
             d = o.matrix(k) - P[k]
             D[k] += d
             touched[k] += (np.abs(d).max(1) > 0)
+            sq[k] += (d.astype(np.float64) ** 2).sum(1)
     for k in mats:
         if how == "sum": P[k] = P[k] + D[k]
         elif how == "avg": P[k] = P[k] + D[k] / R
+        elif how.startswith("sat"): P[k] = P[k] + D[k] / WCS[k][:, None].astype(np.float32)
+        elif how == "adapt":  # w2v_group ADAPTIVE: c = max(1, |sum D|^2 / sum |D|^2) per row
+            coh = (D[k].astype(np.float64) ** 2).sum(1) / np.maximum(sq[k], 1e-30)
+            P[k] = P[k] + D[k] / np.maximum(1.0, coh)[:, None].astype(np.float32)
         elif how.startswith("cap"):  # scale 1 / max(1, c / S) with S = int(how[3:])
             S = float(how[3:])
             P[k] = P[k] + D[k] / np.maximum(1, touched[k] / S)[:, None]

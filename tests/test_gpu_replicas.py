@@ -27,7 +27,8 @@ def _pair_of_handles(mode="sg_ns", dim=72):
     return o, [device_from_oracle(o, cfg, initial=False) for _ in range(2)]
 
 
-@pytest.mark.parametrize("gmode", ["row_average", "sum", "average", "adaptive", "split_all", "split_none"])
+@pytest.mark.parametrize("gmode", ["row_average", "sum", "average", "adaptive", "split_all", "split_none",
+                                   "saturation"])
 @pytest.mark.parametrize("overlap", [False, True])
 @pytest.mark.parametrize("mode", ["sg_ns", "cbow_hs"])
 def test_group_exchange(mode, overlap, gmode):
@@ -36,18 +37,38 @@ def test_group_exchange(mode, overlap, gmode):
     M0 + (M1 - M0) + (M2 - M0) (sum), (M1 + M2) / 2 (average), per row the
     mean of the changes of the replicas that changed it (row_average), or per
     row the sum of the changes divided by max(1, |sum|^2 / sum of |change|^2)
-    (adaptive). Replica 1's changes of rows 0 mod 4 equal replica 0's (a row
-    both moved the same way: adaptive takes their mean there)."""
+    (adaptive), or per row the sum divided by R(1-(1-b)^u)/(1-(1-b)^(Ru)) from
+    the rows' expected updates u per round (saturation; divisors recomputed
+    here from the handle's row update rates). Replica 1's changes of rows 0
+    mod 4 equal replica 0's (a row both moved the same way: adaptive takes
+    their mean there)."""
     o, ds = _pair_of_handles(mode)
     rng = np.random.default_rng(3)
     M0 = [None if m is None else rng.standard_normal(m.shape).astype(np.float32) for m in ds[0].download_model()]
     for d in ds:
         d.upload_model(*M0)
-    g = NativeAverager(ds, overlap=overlap, mode=gmode if not gmode.startswith("split") else "sum")
+    g = NativeAverager(ds, overlap=overlap, mode=gmode if gmode in ("row_average", "sum", "average", "adaptive")
+                       else "sum")
     if gmode.startswith("split"):  # every row saturated (-> the mean) or none (-> the sum)
         n_avg = g.set_split(1000, 0.0 if gmode == "split_all" else 1e30)
         rows = sum(m.shape[0] for m in M0 if m is not None)
         assert n_avg == (rows if gmode == "split_all" else 0)
+    sat_div = []
+    if gmode == "saturation":  # tokens per round chosen so the divisors span (1, 2)
+        tpr, beta = 20_000, 0.01
+        n_div = g.set_saturation(tpr, beta)
+        for k, m in enumerate(M0):
+            if m is None:
+                sat_div.append(None)
+                continue
+            u = ds[0].row_update_rates(k, m.shape[0]) * tpr
+            a, b = -np.expm1(u * np.log1p(-beta)), -np.expm1(2 * u * np.log1p(-beta))
+            want_c = np.clip(np.where(b > 0, 2 * a / np.where(b > 0, b, 1), 1.0), 1.0, 2.0)
+            got_c = g.row_divisors(k, m.shape[0])
+            np.testing.assert_allclose(got_c, want_c, rtol=1e-6)
+            sat_div.append(got_c.astype(np.float64)[:, None])
+        assert 0 < n_div, "some rows must be divided"
+        assert any(float(c.min()) < 1.01 for c in sat_div if c is not None), "and some rows summed"
     info = g.info()
     assert info["local"] and info["nranks"] == 2 and info["overlap"] == overlap
     mats = []
@@ -74,6 +95,9 @@ def test_group_exchange(mode, overlap, gmode):
             want.append((a + b) / 2)
         elif gmode in ("sum", "split_none"):
             want.append(a + b - z)
+        elif gmode == "saturation":
+            c = sat_div[len(want)]
+            want.append(z + ((a - z).astype(np.float64) + (b - z)) / c)
         elif gmode == "adaptive":
             da, db = (a - z).astype(np.float64), (b - z).astype(np.float64)
             tot = da + db

@@ -148,10 +148,15 @@ def train(args, R, rounds, gmode, overlap, seed, data, dev):
         t.set_train_words(max(1, int(args.raw_tokens) // R))
         t.set_rng(N.W2V_RNG_PHILOX, (seed << 32) | 0x5EED)
         t.set_schedule(N.W2V_SCHED_PARALLEL)
+        if args.max_waves > 0:  # the same total concurrency for every R
+            t.set_max_waves(max(1, args.max_waves // R))
         reps.append(t)
     g = None
     if R > 1:
-        if gmode.startswith("split"):  # split<n*>: mean for rows saturated within a round (>= n* updates)
+        if gmode.startswith("sat"):  # sat<beta>: W2V_GROUP_SATURATION
+            g = NativeAverager(reps, overlap=overlap, mode="sum")
+            g.split_rows = g.set_saturation(max(1, int(args.raw_tokens) // R // rounds), float(gmode[3:]))
+        elif gmode.startswith("split"):  # split<n*>: mean for rows saturated within a round (>= n* updates)
             g = NativeAverager(reps, overlap=overlap, mode="sum")
             g.split_rows = g.set_split(max(1, int(args.raw_tokens) // R // rounds), float(gmode[5:]))
         else:
@@ -211,6 +216,7 @@ def main():
     ap.add_argument("--planted-frac", type=float, default=0.10)
     ap.add_argument("--hot-rows", type=int, default=0, help="hot rows exchanged between the full exchanges (0 = none)")
     ap.add_argument("--hot-rounds", type=int, default=0, help="hot-row exchanges per epoch")
+    ap.add_argument("--max-waves", type=int, default=0, help="cap the waves of all R replicas together (each gets max_waves // R; 0 = full chip each)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     t0 = time.time()
@@ -221,7 +227,8 @@ def main():
     del tok
     print(json.dumps({"corpus_tokens": int(args.raw_tokens), "in_vocab": int(ids.size), "V": int(counts.size),
                       "sentences": int(n_sent), "gen_s": round(time.time() - t0, 1), "mode": args.mode,
-                      "dim": args.dim, "iters": args.iters, "planted_frac": args.planted_frac}), flush=True)
+                      "dim": args.dim, "iters": args.iters, "planted_frac": args.planted_frac,
+                      "max_waves": args.max_waves}), flush=True)
     data = (ids, soff, counts, words, args.mode)
     for seed in [int(s) for s in args.seeds.split(",")]:
         hr = args.hot_rows

@@ -27,6 +27,7 @@ W2V_GROUP_AVERAGE = 1
 W2V_GROUP_ROW_AVERAGE = 2
 W2V_GROUP_ADAPTIVE = 3
 W2V_GROUP_SPLIT = 4
+W2V_GROUP_SATURATION = 5
 W2V_RNG_PHILOX = 0
 W2V_RNG_REPLAY = 1
 W2V_SCHED_PARALLEL = 0
@@ -128,6 +129,9 @@ SIGNATURES = {
     "w2v_group_set_overlap": (C.c_int, [_P, _I32]),
     "w2v_group_set_mode": (C.c_int, [_P, _I32]),
     "w2v_group_set_split": (C.c_int, [_P, _I64, _F]),
+    "w2v_group_set_saturation": (C.c_int, [_P, _I64, _F]),
+    "w2v_group_row_divisors": (C.c_int, [_P, _I32, C.POINTER(_F), _I64]),
+    "w2v_dev_row_update_rates": (C.c_int, [_P, _I32, C.POINTER(C.c_double), _I64]),
     "w2v_group_split_rows": (C.c_int, [_P, C.POINTER(_I64)]),
     "w2v_group_average_async": (C.c_int, [_P]),
     "w2v_group_average_rows_async": (C.c_int, [_P, _I64]),

@@ -1490,6 +1490,16 @@ int w2v_dev_private_rate_used(w2v_dev* h, float* mu) {
   return W2V_OK;
 }
 
+int w2v_dev_row_update_rates(w2v_dev* h, int32_t which, double* out, int64_t n) {
+  if (!h || !out) return fail(W2V_ERR_ARG, "null argument");
+  if (which < 0 || which > 2) return fail(W2V_ERR_ARG, "which must be 0 (W), 1 (C) or 2 (synapses1)");
+  std::vector<double> rate;
+  if (!w2v::row_update_rates(h, which, rate)) return fail(W2V_ERR_STATE, "no vocab / corpus statistics uploaded");
+  if (n != (int64_t)rate.size()) return fail(W2V_ERR_ARG, "n must be the matrix's row count");
+  std::copy(rate.begin(), rate.end(), out);
+  return W2V_OK;
+}
+
 int w2v_dev_flush_policy(w2v_dev* h, int32_t* flush_centers, int32_t* context_flush) {
   if (!h) return fail(W2V_ERR_ARG, "null handle");
   if (flush_centers) *flush_centers = h->last_flush;

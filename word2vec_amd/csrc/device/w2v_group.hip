@@ -51,6 +51,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -210,7 +211,7 @@ struct Member {
   float* A[3] = {nullptr, nullptr, nullptr};    // sum over replicas of D (same device: replica 0's only)
   float* F[3] = {nullptr, nullptr, nullptr};    // rows this replica changed (ROW_AVERAGE)
   float* FA[3] = {nullptr, nullptr, nullptr};   // contributors per row, summed (same device: replica 0's only)
-  float* WC[3] = {nullptr, nullptr, nullptr};   // W2V_GROUP_SPLIT: per-row divisor (1 or nranks)
+  float* WC[3] = {nullptr, nullptr, nullptr};   // W2V_GROUP_SPLIT / SATURATION: per-row divisor in [1, nranks]
 };
 
 }  // namespace
@@ -227,10 +228,11 @@ struct w2v_group {
   bool pending = false;     // an overlapped exchange is in flight
   int64_t elems[3] = {0, 0, 0};  // floats per matrix (rows x pitch), 0 = unused
   int64_t rounds = 0;       // exchanges issued
-  int64_t split_rows = 0;   // W2V_GROUP_SPLIT: rows (all matrices) averaged instead of summed
+  int64_t split_rows = 0;   // W2V_GROUP_SPLIT / SATURATION: rows (all matrices) with a divisor > 1
   float scale() const { return mode == W2V_GROUP_AVERAGE ? 1.0f / (float)nranks : 1.0f; }
   bool rows_counted() const { return mode == W2V_GROUP_ROW_AVERAGE || mode == W2V_GROUP_ADAPTIVE; }
   bool adaptive() const { return mode == W2V_GROUP_ADAPTIVE; }
+  bool row_divisors() const { return mode == W2V_GROUP_SPLIT || mode == W2V_GROUP_SATURATION; }
   int64_t rows(int k) const { return pitch > 0 ? elems[k] / pitch : 0; }
   // Rows each exchange covers (w2v_group_average_rows_async): matrix k's rows
   // [lo[k], lo[k] + n[k]); `cur` for the exchange being issued, `pend` for the
@@ -286,7 +288,7 @@ const float* sum_of(const w2v_group* g, size_t i, int k, const w2v_group::Span& 
   return (g->local ? g->m[0].A[k] : g->m[i].A[k]) + g->at(sp, k);
 }
 const float* count_of(const w2v_group* g, size_t i, int k, const w2v_group::Span& sp) {
-  if (g->mode == W2V_GROUP_SPLIT) return g->m[i].WC[k] + sp.lo[k];
+  if (g->row_divisors()) return g->m[i].WC[k] + sp.lo[k];
   if (!g->rows_counted()) return nullptr;
   return (g->local ? g->m[0].FA[k] : g->m[i].FA[k]) + sp.lo[k];
 }
@@ -566,23 +568,24 @@ int w2v_group_set_mode(w2v_group* g, int32_t mode) {
   return W2V_OK;
 }
 
-int w2v_group_set_split(w2v_group* g, int64_t tokens_per_round, float saturated_updates) {
-  w2v::Range range_("w2v_group_set_split");
-  if (!g) return fail_g(W2V_ERR_ARG, "null group");
-  if (tokens_per_round < 1 || !(saturated_updates >= 0.0f))
-    return fail_g(W2V_ERR_ARG, "w2v_group_set_split: tokens_per_round >= 1 and saturated_updates >= 0");
-  if (g->pending) return fail_g(W2V_ERR_STATE, "w2v_group_set_split: an exchange is in flight (w2v_group_finish first)");
-  // the per-row divisors from member 0's corpus statistics (every replica
-  // trains the same vocabulary on a shard of the same corpus)
+}  // extern "C"
+
+namespace {
+// Per-row divisors of the summed update from member 0's corpus statistics
+// (every replica trains the same vocabulary on a shard of the same corpus):
+// c = divisor(u), u = the row's expected updates per replica in a round of
+// tokens_per_round raw tokens.
+template <class F>
+int set_row_divisors(w2v_group* g, int64_t tokens_per_round, int32_t mode, F divisor, const char* what) {
+  if (g->pending) return fail_g(W2V_ERR_STATE, std::string(what) + ": an exchange is in flight (w2v_group_finish first)");
   std::vector<float> wc[3];
   for (int k = 0; k < 3; ++k) {
     if (!g->elems[k]) continue;
     std::vector<double> rate;
     if (!w2v::row_update_rates(g->m[0].h, k, rate) || (int64_t)rate.size() != g->rows(k))
-      return fail_g(W2V_ERR_STATE, "w2v_group_set_split: the replicas need their vocab and corpus statistics uploaded");
+      return fail_g(W2V_ERR_STATE, std::string(what) + ": the replicas need their vocab and corpus statistics uploaded");
     wc[k].resize(rate.size());
-    for (size_t r = 0; r < rate.size(); ++r)
-      wc[k][r] = rate[r] * (double)tokens_per_round >= (double)saturated_updates ? (float)g->nranks : 1.0f;
+    for (size_t r = 0; r < rate.size(); ++r) wc[k][r] = divisor(rate[r] * (double)tokens_per_round);
   }
   for (auto& x : g->m) {
     HIP_G(hipSetDevice(x.device));
@@ -596,8 +599,43 @@ int w2v_group_set_split(w2v_group* g, int64_t tokens_per_round, float saturated_
   for (int k = 0; k < 3; ++k)
     for (float w : wc[k]) avg += w > 1.0f;
   g->split_rows = avg;
-  g->mode = W2V_GROUP_SPLIT;
+  g->mode = mode;
   return W2V_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int w2v_group_set_split(w2v_group* g, int64_t tokens_per_round, float saturated_updates) {
+  w2v::Range range_("w2v_group_set_split");
+  if (!g) return fail_g(W2V_ERR_ARG, "null group");
+  if (tokens_per_round < 1 || !(saturated_updates >= 0.0f))
+    return fail_g(W2V_ERR_ARG, "w2v_group_set_split: tokens_per_round >= 1 and saturated_updates >= 0");
+  const float R = (float)g->nranks;
+  return set_row_divisors(g, tokens_per_round, W2V_GROUP_SPLIT,
+                          [&](double u) { return u >= (double)saturated_updates ? R : 1.0f; }, "w2v_group_set_split");
+}
+
+// W2V_GROUP_SATURATION. A row that one model would update n times in a round,
+// each update contracting its distance to the row's current optimum by a
+// factor (1 - beta), moves 1 - (1 - beta)^n of the way; R replicas that each
+// update it u = n / R times from the same start move R (1 - (1 - beta)^u) in
+// sum. The divisor c = R (1 - (1 - beta)^u) / (1 - (1 - beta)^(R u)) makes the
+// exchanged move the one model's: c -> 1 (the sum) for rows in the linear
+// regime (u beta << 1: independent small updates add), c -> R (the mean) for
+// rows every replica drives to the same optimum within the round (summing R
+// such moves overshoots R-fold, which is GD past its stability bound for R > 2).
+int w2v_group_set_saturation(w2v_group* g, int64_t tokens_per_round, float beta) {
+  w2v::Range range_("w2v_group_set_saturation");
+  if (!g) return fail_g(W2V_ERR_ARG, "null group");
+  if (tokens_per_round < 1 || !(beta > 0.0f && beta < 1.0f))
+    return fail_g(W2V_ERR_ARG, "w2v_group_set_saturation: tokens_per_round >= 1 and 0 < beta < 1");
+  const double R = (double)g->nranks, lb = std::log1p(-(double)beta);
+  return set_row_divisors(g, tokens_per_round, W2V_GROUP_SATURATION, [&](double u) {
+    const double a = -std::expm1(u * lb), b = -std::expm1(R * u * lb);
+    const double c = b > 0.0 ? R * a / b : 1.0;
+    return (float)std::min(R, std::max(1.0, c));
+  }, "w2v_group_set_saturation");
 }
 
 int w2v_group_average_async(w2v_group* g) {
@@ -634,9 +672,22 @@ int w2v_group_finish(w2v_group* g) {
   return W2V_OK;
 }
 
+int w2v_group_row_divisors(w2v_group* g, int32_t which, float* out, int64_t n) {
+  if (!g || !out) return fail_g(W2V_ERR_ARG, "null argument");
+  if (which < 0 || which > 2 || !g->elems[which]) return fail_g(W2V_ERR_ARG, "no such matrix in the group");
+  if (n != g->rows(which)) return fail_g(W2V_ERR_ARG, "n must be the matrix's row count");
+  if (!g->row_divisors()) {
+    std::fill(out, out + n, 1.0f);
+    return W2V_OK;
+  }
+  HIP_G(hipSetDevice(g->m[0].device));
+  HIP_G(hipMemcpy(out, g->m[0].WC[which], (size_t)n * sizeof(float), hipMemcpyDeviceToHost));
+  return W2V_OK;
+}
+
 int w2v_group_split_rows(w2v_group* g, int64_t* rows) {
   if (!g || !rows) return fail_g(W2V_ERR_ARG, "null argument");
-  *rows = g->mode == W2V_GROUP_SPLIT ? g->split_rows : 0;
+  *rows = g->row_divisors() ? g->split_rows : 0;
   return W2V_OK;
 }
 

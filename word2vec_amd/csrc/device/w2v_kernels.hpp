@@ -786,7 +786,11 @@ __device__ __forceinline__ void sg_center(const TrainArgs& a, float* lds, const 
       int ta = 0, tb = 0;
       const int T1 = ns_targets(neg, readlane_i(cw_l, k), negw_l, gs * neg, lane, ta);
       const int T2 = (k + 1 < nctx) ? ns_targets(neg, readlane_i(cw_l, k + 1), negw_l, (gs + 1) * neg, lane, tb) : 0;
-      const int tgt_l = lane < kPairHalf ? ta : __shfl(tb, (lane - kPairHalf) & (kWave - 1));
+      // every lane takes part in the permute: a lane whose exec bit is off
+      // supplies no data to ds_bpermute, so a shuffle under `lane >= kPairHalf`
+      // would read B's targets from switched-off lanes 0..5
+      const int tb_s = __shfl(tb, (lane - kPairHalf) & (kWave - 1));
+      const int tgt_l = lane < kPairHalf ? ta : tb_s;
       if (a.strict) drain_vmem();
       apply_pair<NV>(a, a.C, T1, T2, tgt_l, lane, x, g, alpha, pr);
       cnt.targets += (unsigned long long)(T1 + T2);

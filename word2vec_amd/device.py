@@ -253,6 +253,13 @@ class DeviceTrainer:
         self._chk(self.lib.w2v_dev_set_context_private(self.h, int(rows), int(flush_centers)),
                   "w2v_dev_set_context_private")
 
+    def row_update_rates(self, which: int, rows: int) -> np.ndarray:
+        """Expected updates per raw token of each row of matrix `which` (0 W, 1 C, 2 synapses1)."""
+        out = np.empty(rows, np.float64)
+        self._chk(self.lib.w2v_dev_row_update_rates(self.h, int(which), out.ctypes.data_as(C.POINTER(C.c_double)),
+                                                    int(rows)), "w2v_dev_row_update_rates")
+        return out
+
     def set_max_waves(self, n: int):
         """Cap on wavefronts in flight (0 = as many as fit)."""
         self._chk(self.lib.w2v_dev_set_max_waves(self.h, int(n)), "w2v_dev_set_max_waves")

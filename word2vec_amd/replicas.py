@@ -128,6 +128,26 @@ class NativeAverager:
         self.N.check(self.lib, self.lib.w2v_group_split_rows(self.g, C.byref(n)), "w2v_group_split_rows")
         return n.value
 
+    def set_saturation(self, tokens_per_round: int, beta: float) -> int:
+        """W2V_GROUP_SATURATION: the summed update divided per row by R(1-(1-beta)^u)/(1-(1-beta)^(Ru)), u =
+        the row's expected updates per replica in a round of tokens_per_round tokens (the sum for rarely
+        updated rows, the mean for rows every replica saturates within the round). Returns the rows with a
+        divisor above 1."""
+        self.N.check(self.lib, self.lib.w2v_group_set_saturation(self.g, int(tokens_per_round), float(beta)),
+                     "w2v_group_set_saturation")
+        n = C.c_int64()
+        self.N.check(self.lib, self.lib.w2v_group_split_rows(self.g, C.byref(n)), "w2v_group_split_rows")
+        return n.value
+
+    def row_divisors(self, which: int, rows: int):
+        """The per-row divisors of matrix `which` the exchange applies (all 1 outside SPLIT / SATURATION)."""
+        import numpy as np
+
+        out = np.empty(rows, np.float32)
+        self.N.check(self.lib, self.lib.w2v_group_row_divisors(self.g, int(which), out.ctypes.data_as(C.POINTER(C.c_float)),
+                                                               int(rows)), "w2v_group_row_divisors")
+        return out
+
     def average(self, rows: int = 0) -> None:
         """Exchange all rows (rows == 0) or only the `rows` hottest (W / C rows [0, rows), the nodes nearest
         the Huffman root)."""
