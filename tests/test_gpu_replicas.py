@@ -54,8 +54,10 @@ def test_group_exchange(mode, overlap, gmode):
         rows = sum(m.shape[0] for m in M0 if m is not None)
         assert n_avg == (rows if gmode == "split_all" else 0)
     sat_div = []
-    if gmode == "saturation":  # tokens per round chosen so the divisors span (1, 2)
-        tpr, beta = 20_000, 0.01
+    if gmode == "saturation":  # tokens per round chosen so the divisors span (1, 2): median u * beta = 1
+        beta = 0.01
+        r0 = ds[0].row_update_rates(0, M0[0].shape[0])
+        tpr = max(1, int(1.0 / (beta * float(np.median(r0[r0 > 0])))))
         n_div = g.set_saturation(tpr, beta)
         for k, m in enumerate(M0):
             if m is None:

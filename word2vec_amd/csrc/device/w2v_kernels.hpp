@@ -629,11 +629,14 @@ __device__ __forceinline__ void apply_list(const TrainArgs& a, float* M, int T, 
 // is unchanged — and A's gradient terms accumulate before B's.
 constexpr int kPairHalf = 6;
 constexpr int kPairNeg = kPairHalf - 1;
-#ifndef W2V_NS_PAIR  // 0: one context per batch (experiments)
-#define W2V_NS_PAIR 1
+#ifndef W2V_NS_PAIR  // 1: two contexts per batch (measured: no gain; off)
+#define W2V_NS_PAIR 0
+#endif
+#ifndef W2V_NS_PAIR_MIN_NV
+#define W2V_NS_PAIR_MIN_NV 3
 #endif
 template <int NV>
-constexpr bool kNsPair = W2V_NS_PAIR && NV >= 3;  // d <= 128 keeps 64 VGPRs (8 waves/SIMD): no room for 12 rows
+constexpr bool kNsPair = W2V_NS_PAIR && NV >= W2V_NS_PAIR_MIN_NV;  // d <= 128 keeps 64 VGPRs (8 waves/SIMD)
 
 template <int NV>
 __device__ __forceinline__ void pair_update(float* M, int64_t pitch, int d, int lane, int row, bool hot, bool priv,
