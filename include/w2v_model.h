@@ -35,6 +35,8 @@ void w2v_model_set_shared_negatives(w2v_model* m, int32_t on);
 /* Word2Vec::gpu_devices / sync_words / overlap_average: n >= 2 devices train
  * data-parallel replicas (a device may repeat); n < 2 = one device. */
 void w2v_model_replicas(w2v_model* m, const int32_t* devices, int32_t n, int64_t sync_words, int32_t overlap);
+/* Word2Vec::replica_mode (a W2V_GROUP_* mode of include/w2v_dev.h). */
+void w2v_model_replica_mode(w2v_model* m, int32_t mode);
 /* Word2Vec::gpu_ingest / ingest_chunk_bytes: count and map corpus files on the
  * GPU (include/w2v_ingest.h) in build_vocab_file / file_samples / train_file. */
 void w2v_model_set_gpu_ingest(w2v_model* m, int32_t on, int64_t chunk_bytes);

@@ -8,6 +8,11 @@ from tests import paired
 from word2vec_amd.evaluate import analogy_accuracy, similarity_score
 name, mode, R, rounds, how = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
 warm = float(sys.argv[6]) if len(sys.argv) > 6 else 0.0
+import os
+_lr = float(os.environ.get("W2V_SIM_LR_SCALE", "1"))
+if _lr != 1.0:  # linear learning-rate scaling with R (large-batch SGD's rule), for the avg exchange
+    _params = paired.params
+    paired.params = lambda *a, **k: dict(_params(*a, **k), init_alpha=_params(*a, **k)["init_alpha"] * _lr)
 sents, qs, pairs = paired.corpus(name)
 o, orders, key, p = paired.setup(name, mode, 1, sents)
 ids, off = o.samples()
@@ -41,14 +46,18 @@ if how.startswith("sat"):  # sat<beta>: smooth saturation-corrected sum (w2v_gro
     qk = fk.sum()
     u_tab = cnt ** 0.75 / (cnt ** 0.75).sum()
     rate = {0: fk, 1: qk * 6.0 * (f + 5 * u_tab)}  # SG-NS per raw token (window 5: win1 = 6 on average... )
-    beta = float(how[3:])
+    beta0 = float(how[4:] if how.startswith("satd") else how[3:])
     tok_round = tw / R / rounds
-    WCS = {}
-    for k in mats:
-        u = rate[k] * tok_round
-        a = -np.expm1(u * np.log1p(-beta))
-        b = -np.expm1(R * u * np.log1p(-beta))
-        WCS[k] = np.where(b > 0, R * a / np.maximum(b, 1e-300), 1.0)
+
+    def divisors(beta):
+        out = {}
+        for k in mats:
+            u = rate[k] * tok_round
+            a = -np.expm1(u * np.log1p(-beta))
+            b = -np.expm1(R * u * np.log1p(-beta))
+            out[k] = np.where(b > 0, R * a / np.maximum(b, 1e-300), 1.0)
+        return out
+    WCS = divisors(beta0)
 for r in range(rounds):
     D = {k: np.zeros_like(P[k]) for k in mats}
     touched = {k: np.zeros(P[k].shape[0]) for k in mats}
@@ -69,6 +78,8 @@ for r in range(rounds):
             D[k] += d
             touched[k] += (np.abs(d).max(1) > 0)
             sq[k] += (d.astype(np.float64) ** 2).sum(1)
+    if how.startswith("satd"):  # beta follows the learning rate (linear decay, as alpha)
+        WCS = divisors(max(beta0 * (1.0 - glob / tw), beta0 * 1e-4))
     for k in mats:
         if how == "sum": P[k] = P[k] + D[k]
         elif how == "avg": P[k] = P[k] + D[k] / R
@@ -82,4 +93,4 @@ for r in range(rounds):
         else: P[k] = P[k] + D[k] / np.maximum(1, touched[k])[:, None]
     glob += sum(int(off[s + 1] - off[s]) for sh in shards for s in sh[len(sh) * r // rounds: len(sh) * (r + 1) // rounds])
 E = P[1 if mode == "cbow_hs" else 0]
-print(name, mode, R, rounds, how, warm, round(analogy_accuracy(words, E, qs)["accuracy"], 2), round(similarity_score(words, E, pairs)["spearman"], 2), flush=True)
+print(name, mode, R, rounds, how + (f"_lr{_lr:g}" if _lr != 1.0 else ""), warm, round(analogy_accuracy(words, E, qs)["accuracy"], 2), round(similarity_score(words, E, pairs)["spearman"], 2), flush=True)

@@ -54,10 +54,10 @@ def test_group_exchange(mode, overlap, gmode):
         rows = sum(m.shape[0] for m in M0 if m is not None)
         assert n_avg == (rows if gmode == "split_all" else 0)
     sat_div = []
-    if gmode == "saturation":  # tokens per round chosen so the divisors span (1, 2): median u * beta = 1
+    if gmode == "saturation":  # tokens per round chosen so the divisors span (1, 2): max u * beta = 5
         beta = 0.01
-        r0 = ds[0].row_update_rates(0, M0[0].shape[0])
-        tpr = max(1, int(1.0 / (beta * float(np.median(r0[r0 > 0])))))
+        rmax = max(float(ds[0].row_update_rates(k, m.shape[0]).max()) for k, m in enumerate(M0) if m is not None)
+        tpr = max(1, int(5.0 / (beta * rmax)))
         n_div = g.set_saturation(tpr, beta)
         for k, m in enumerate(M0):
             if m is None:
@@ -70,7 +70,8 @@ def test_group_exchange(mode, overlap, gmode):
             np.testing.assert_allclose(got_c, want_c, rtol=1e-6)
             sat_div.append(got_c.astype(np.float64)[:, None])
         assert 0 < n_div, "some rows must be divided"
-        assert any(float(c.min()) < 1.01 for c in sat_div if c is not None), "and some rows summed"
+        cs = np.concatenate([c.ravel() for c in sat_div if c is not None])
+        assert float(cs.max()) > 1.5 and float(cs.min()) < 1.2, "divisors must span (1, 2)"
     info = g.info()
     assert info["local"] and info["nranks"] == 2 and info["overlap"] == overlap
     mats = []
@@ -224,7 +225,7 @@ def test_order_slices_equal_one_launch():
     b.close()
 
 
-def _train_class(sents, mode, seed, gpu_devices, sync_words, overlap, max_waves):
+def _train_class(sents, mode, seed, gpu_devices, sync_words, overlap, max_waves, replica_mode="sum"):
     from tests import paired
     from tests.harness import MODES
     from word2vec_amd.model import Word2Vec
@@ -235,7 +236,7 @@ def _train_class(sents, mode, seed, gpu_devices, sync_words, overlap, max_waves)
                  word_dim=p["dim"], negative=m["negative"], subsample_threshold=p["subsample"],
                  init_alpha=p["init_alpha"], min_alpha=2.5e-6, cbow_mean=True, train_method=m["train_method"],
                  model=m["model"], gpu_devices=gpu_devices, sync_words=sync_words, overlap_average=overlap,
-                 max_waves=max_waves)
+                 max_waves=max_waves, replica_mode=replica_mode)
     w.seed(seed)
     w.build_vocab(sents)
     w.init_weights()
@@ -255,7 +256,8 @@ def test_two_replicas_one_gpu_quality(mode):
     """SURVEY.md §4 level 4 through the C++ class (gpu_devices = {0, 0}): two
     replicas, each training half of every epoch's sentences on one wavefront
     (the deterministic schedule: what is measured is the exchange, not the
-    Hogwild policy), summing their updates every 1/64 epoch, against one
+    Hogwild policy), summing their updates every 1/64 epoch (replica_mode
+    sum: on a 2 M-token corpus the mean halves what each row learns), against one
     replica training all of them, at equal tokens (text8-like corpus, 2 M
     tokens)."""
     from tests import paired

@@ -7,7 +7,7 @@
 // the pre-override 0.025 (:116), 1000-token sentences (:66), and which matrix
 // is written (:196-201). Additive: -train is honoured (the reference always
 // reads ./text8), -binary, -gpu, -replay, -shared-negatives, and the
-// multi-GPU flags -gpus, -sync-words, -overlap (Word2Vec::gpu_devices), -gpu-ingest.
+// multi-GPU flags -gpus, -sync-words, -overlap, -replica-mode (Word2Vec::gpu_devices), -gpu-ingest.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -43,6 +43,7 @@ void usage() {
                "  -gpus <int>           data-parallel replicas on devices gpu .. gpu+n-1, averaged with RCCL (default 1)\n"
                "  -sync-words <int>     average the replicas every this many words of a shard (default 0: per epoch)\n"
                "  -overlap <0|1>        overlap the averaging with the next round's training (default 1)\n"
+               "  -replica-mode <sum|average|row_average|adaptive> how the replicas' updates combine (default average)\n"
                "  -gpu-ingest <0|1>     count and map the corpus on the GPU (default 0: host threads)\n\n"
                "example: ./word2vec -train text8 -output vec.txt -size 300 -window 5 -subsample 1e-4 "
                "-negative 5 -model sg -train_method ns -iter 3\n";
@@ -75,6 +76,7 @@ int main(int argc, char** argv) {
   const bool cbow_mean = true;
   int binary = 0, gpu = 0, replay = 0, shared = 0, gpus = 1, overlap = 1, gpu_ingest = 0;
   long long sync_words = 0;
+  std::string replica_mode = "average";
   int i;
   if ((i = find_flag("-size", argc, argv)) > 0) word_dim = std::atoi(argv[i + 1]);
   if ((i = find_flag("-train", argc, argv)) > 0) input_file = argv[i + 1];
@@ -97,9 +99,20 @@ int main(int argc, char** argv) {
   if ((i = find_flag("-gpus", argc, argv)) > 0) gpus = std::atoi(argv[i + 1]);
   if ((i = find_flag("-sync-words", argc, argv)) > 0) sync_words = std::atoll(argv[i + 1]);
   if ((i = find_flag("-overlap", argc, argv)) > 0) overlap = std::atoi(argv[i + 1]);
+  if ((i = find_flag("-replica-mode", argc, argv)) > 0) replica_mode = argv[i + 1];
   if ((i = find_flag("-gpu-ingest", argc, argv)) > 0) gpu_ingest = std::atoi(argv[i + 1]);
   if (gpus < 1 || sync_words < 0) {
     std::cout << "Please set -gpus >= 1 and -sync-words >= 0!" << std::endl;
+    return 1;
+  }
+  int replica_mode_id = -1;
+  {
+    const char* names[] = {"sum", "average", "row_average", "adaptive"};
+    for (int k = 0; k < 4; ++k)
+      if (replica_mode == names[k]) replica_mode_id = k;  // W2V_GROUP_SUM .. W2V_GROUP_ADAPTIVE
+  }
+  if (replica_mode_id < 0) {
+    std::cout << "Please set -replica-mode to sum, average, row_average or adaptive!" << std::endl;
     return 1;
   }
 
@@ -155,6 +168,7 @@ int main(int argc, char** argv) {
     for (int k = 0; k < gpus; ++k) w2v.gpu_devices.push_back(gpu + k);
   w2v.sync_words = sync_words;
   w2v.overlap_average = overlap != 0;
+  w2v.replica_mode = replica_mode_id;
   w2v.gpu_ingest = gpu_ingest != 0;
   // main.cpp:63-92's reader (1000-token sentences), streamed from the mapped
   // file by host threads: the same vocabulary and samples as building

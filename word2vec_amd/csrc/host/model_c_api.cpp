@@ -102,6 +102,8 @@ void w2v_model_replicas(w2v_model* m, const int32_t* devices, int32_t n, int64_t
   m->w.overlap_average = overlap != 0;
 }
 
+void w2v_model_replica_mode(w2v_model* m, int32_t mode) { m->w.replica_mode = mode; }
+
 void w2v_model_set_gpu_ingest(w2v_model* m, int32_t on, int64_t chunk_bytes) {
   m->w.gpu_ingest = on != 0;
   m->w.ingest_chunk_bytes = chunk_bytes > 0 ? chunk_bytes : 0;

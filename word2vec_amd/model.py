@@ -14,6 +14,8 @@ import numpy as np
 from .host import HOST_LIB
 
 _lib = None
+# Word2Vec::replica_mode values (include/w2v_dev.h W2V_GROUP_*)
+REPLICA_MODES = {"sum": 0, "average": 1, "row_average": 2, "adaptive": 3}
 
 
 def _load():
@@ -33,6 +35,7 @@ def _load():
             "w2v_model_context_policy": (None, [P, I32, I32]),
             "w2v_model_set_shared_negatives": (None, [P, I32]),
             "w2v_model_replicas": (None, [P, P, I32, I64, I32]),
+            "w2v_model_replica_mode": (None, [P, I32]),
             "w2v_model_set_gpu_ingest": (None, [P, I32, I64]),
             "w2v_model_build_vocab": (C.c_int, [P, S, I64]),
             "w2v_model_train": (C.c_int, [P, S, I64]),
@@ -92,7 +95,7 @@ class Word2Vec:
                  train_method="hs", model="cbow", gpu_device=0, replay_rng=False, verbose=False, hot_rows=-2,
                  private_rows=-1, flush_centers=0, private_average=8.0, max_waves=0, shared_negatives=False,
                  context_rows=-1, context_flush=0, gpu_devices=None, sync_words=0, overlap_average=True,
-                 gpu_ingest=False, ingest_chunk_bytes=0, checkpoint_path=""):
+                 replica_mode="average", gpu_ingest=False, ingest_chunk_bytes=0, checkpoint_path=""):
         self.L = _load()
         self.word_dim = word_dim
         self.h = self.L.w2v_model_new(iter, window, min_count, table_size, word_dim, negative, subsample_threshold,
@@ -108,6 +111,7 @@ class Word2Vec:
         if gpu_devices:
             devs = np.ascontiguousarray(gpu_devices, np.int32)
             self.L.w2v_model_replicas(self.h, _p(devs), devs.size, int(sync_words), int(bool(overlap_average)))
+            self.L.w2v_model_replica_mode(self.h, REPLICA_MODES[replica_mode])
         self.L.w2v_model_set_gpu_ingest(self.h, int(bool(gpu_ingest)), int(ingest_chunk_bytes))
         if checkpoint_path:
             self.set_checkpoint_path(checkpoint_path)
