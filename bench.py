@@ -93,6 +93,9 @@ def parse():
                     help="N=1 only: let the library allocate the matrices instead of torch")
     ap.add_argument("--sync-every", type=int, default=0,
                     help="average the replicas every this many sentences of a shard (0 = once per step)")
+    ap.add_argument("--replica-mode", default="auto", choices=["auto", "sum", "average", "row_average", "adaptive"],
+                    help="N>1: how the replicas' updates combine (auto: sum for 2 ranks, average for more, "
+                         "as Word2Vec::replica_mode; DESIGN.md §6)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N>1: average the replicas in place on the training stream instead of from a snapshot "
                          "on a communication stream overlapped with the next round")
@@ -239,9 +242,11 @@ def main():
     if world > 1 and not share:
         uid = [group_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        averager = NativeAverager([tr], uid[0], world, rank, overlap=not args.no_overlap)
+        rmode = args.replica_mode if args.replica_mode != "auto" else ("sum" if world <= 2 else "average")
+        averager = NativeAverager([tr], uid[0], world, rank, overlap=not args.no_overlap, mode=rmode)
     else:  # N = 1 (no-op) or the one-GPU rehearsal (ranks share cuda:0: RCCL needs one rank per GPU)
         averager = TorchAverager(mats, world)
+    rmode_used = (args.replica_mode if args.replica_mode != "auto" else ("sum" if world <= 2 else "average"))
     rounds = n_rounds(n_sent * world, world, args.sync_every)
     order_dev = torch.arange(n_sent, dtype=torch.int64, device=dev)  # this rank's shard, in order
     round_words = global_round_words(local_round_words(soff_h, range(n_sent), rounds), world)
@@ -355,8 +360,9 @@ def main():
                 "vocab_size": V,
                 "global_batch": n_tok * world,
                 "parallelism": (f"dp{world}: full replica per GPU, corpus shard per GPU, RCCL all-reduce "
-                                f"average (w2v_group, {'overlapped' if not args.no_overlap else 'blocking'}) "
-                                f"x{rounds} per step" if world > 1 else "dp1"),
+                                f"of the updates, {rmode_used} (w2v_group, "
+                                f"{'overlapped' if not args.no_overlap else 'blocking'}) x{rounds} per step"
+                                if world > 1 else "dp1"),
                 "hot_rows": args.hot_rows,
                 "private_rows": args.private_rows,
                 "flush_centers": args.flush_centers,

@@ -113,14 +113,19 @@ class Word2Vec {
   // Data-parallel replicas (BASELINE configs[3]): with >= 2 entries, train()
   // runs one full model replica per listed HIP device (a device may repeat:
   // replicas sharing one GPU), each on a contiguous shard of every epoch's
-  // shuffled sentence order, and averages them (include/w2v_dev.h w2v_group_*:
-  // RCCL all-reduce over xGMI) every sync_words in-vocab words of the largest
-  // shard (0 = once per epoch), overlapped with the next round's training
-  // unless overlap_average is false. Empty = one device (gpu_device).
+  // shuffled sentence order, and exchanges their updates (include/w2v_dev.h
+  // w2v_group_*: RCCL all-reduce over xGMI) every sync_words in-vocab words of
+  // the largest shard (0 = auto: kAutoReplicaRounds exchanges per epoch),
+  // overlapped with the next round's training unless overlap_average is false.
+  // replica_mode: a W2V_GROUP_* mode, or -1 = auto: W2V_GROUP_SUM for two
+  // replicas, W2V_GROUP_AVERAGE (model averaging) for more — summing R >= 3
+  // replicas' updates overshoots the frequent rows R-fold and diverges
+  // (DESIGN.md §6 has the measured table). Empty = one device (gpu_device).
   std::vector<int> gpu_devices;
   int64_t sync_words = 0;
   bool overlap_average = true;
-  int replica_mode = W2V_GROUP_SUM;  // w2v_group_set_mode: how the replicas' updates combine
+  int replica_mode = -1;
+  static const int64_t kAutoReplicaRounds = 64;  // 2 replicas within a point at 32-64 per epoch
   bool verbose = true;       // progress line per epoch (the reference prints one
                              // every 100 sentences, Word2Vec.cpp:382-386)
   // Train on a corpus that is already token ids (no strings): ids index

@@ -225,7 +225,7 @@ def test_order_slices_equal_one_launch():
     b.close()
 
 
-def _train_class(sents, mode, seed, gpu_devices, sync_words, overlap, max_waves, replica_mode="sum"):
+def _train_class(sents, mode, seed, gpu_devices, sync_words, overlap, max_waves, replica_mode="auto"):
     from tests import paired
     from tests.harness import MODES
     from word2vec_amd.model import Word2Vec
@@ -253,21 +253,20 @@ REPLICA_BOUND = {"cbow_hs": 1.0, "sg_ns": 1.0}
 
 @pytest.mark.parametrize("mode", ["sg_ns", "cbow_hs"])
 def test_two_replicas_one_gpu_quality(mode):
-    """SURVEY.md §4 level 4 through the C++ class (gpu_devices = {0, 0}): two
-    replicas, each training half of every epoch's sentences on one wavefront
-    (the deterministic schedule: what is measured is the exchange, not the
-    Hogwild policy), summing their updates every 1/64 epoch (replica_mode
-    sum: on a 2 M-token corpus the mean halves what each row learns), against one
-    replica training all of them, at equal tokens (text8-like corpus, 2 M
-    tokens)."""
+    """SURVEY.md §4 level 4 through the C++ class (gpu_devices = {0, 0}) with
+    the class's default exchange settings (replica_mode auto = sum for two
+    replicas, sync_words 0 = 64 exchanges per epoch): two replicas, each
+    training half of every epoch's sentences on one wavefront (the
+    deterministic schedule: what is measured is the exchange, not the Hogwild
+    policy), against one replica training all of them, at equal tokens
+    (text8-like corpus, 2 M tokens)."""
     from tests import paired
     from word2vec_amd.evaluate import analogy_accuracy, similarity_score
 
     sents, qs, pairs = paired.corpus("text8_small")
-    sync = sum(len(s) for s in sents) // 2 // 64
     res = {}
     for name, devs in (("one", None), ("two", [0, 0])):
-        words, E = _train_class(sents, mode, 1, devs, sync, False, 1)
+        words, E = _train_class(sents, mode, 1, devs, 0, False, 1)
         assert np.isfinite(E).all()
         res[name] = np.array([analogy_accuracy(words, E, qs)["accuracy"], similarity_score(words, E, pairs)["spearman"]])
     d = res["two"] - res["one"]

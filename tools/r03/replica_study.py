@@ -137,8 +137,9 @@ def train(args, R, rounds, gmode, overlap, seed, data, dev):
     C0 = ((rng.random((V, d), dtype=np.float32) - 0.5) / d).astype(np.float32) if hs else \
         (np.zeros((V, d), np.float32) if (neg or cbow) else None)
     S0 = np.zeros((V - 1, d), np.float32) if hs else None
+    a0 = (0.05 if cbow else 0.025) * (args.lr_scale if R > 1 else 1.0)  # linear LR scaling of the replicas
     cfg = Config(word_dim=d, window=5, negative=neg, hs=hs, cbow=cbow, cbow_mean=True, iter=args.iters,
-                 init_alpha=0.05 if cbow else 0.025, min_alpha=2.5e-6, table_size=100_000_000, device=0)
+                 init_alpha=a0, min_alpha=2.5e-6, table_size=100_000_000, device=0)
     reps = []
     for _ in range(R):
         t = DeviceTrainer(cfg)
@@ -216,6 +217,7 @@ def main():
     ap.add_argument("--planted-frac", type=float, default=0.10)
     ap.add_argument("--hot-rows", type=int, default=0, help="hot rows exchanged between the full exchanges (0 = none)")
     ap.add_argument("--hot-rounds", type=int, default=0, help="hot-row exchanges per epoch")
+    ap.add_argument("--lr-scale", type=float, default=1.0, help="init_alpha x this for R > 1 (linear scaling rule)")
     ap.add_argument("--max-waves", type=int, default=0, help="cap the waves of all R replicas together (each gets max_waves // R; 0 = full chip each)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -228,7 +230,7 @@ def main():
     print(json.dumps({"corpus_tokens": int(args.raw_tokens), "in_vocab": int(ids.size), "V": int(counts.size),
                       "sentences": int(n_sent), "gen_s": round(time.time() - t0, 1), "mode": args.mode,
                       "dim": args.dim, "iters": args.iters, "planted_frac": args.planted_frac,
-                      "max_waves": args.max_waves}), flush=True)
+                      "max_waves": args.max_waves, "lr_scale": args.lr_scale}), flush=True)
     data = (ids, soff, counts, words, args.mode)
     for seed in [int(s) for s in args.seeds.split(",")]:
         hr = args.hot_rows

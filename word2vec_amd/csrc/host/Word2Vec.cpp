@@ -554,7 +554,9 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
     }
     check(w2v_group_create(reps.data(), (int32_t)R, nullptr, (int32_t)R, 0, &grp), "w2v_group_create");
     check(w2v_group_set_overlap(grp, overlap_average ? 1 : 0), "w2v_group_set_overlap");
-    check(w2v_group_set_mode(grp, replica_mode), "w2v_group_set_mode");
+    const int mode = replica_mode >= 0 ? replica_mode : (R <= 2 ? W2V_GROUP_SUM : W2V_GROUP_AVERAGE);
+    const int64_t auto_rounds = kAutoReplicaRounds;
+    check(w2v_group_set_mode(grp, mode), "w2v_group_set_mode");
     std::vector<long> sample_idx((size_t)n);
     std::iota(sample_idx.begin(), sample_idx.end(), 0);
     int64_t global = cont ? start_words_ : 0;  // the reference's current_words over all replicas (:359, :393)
@@ -576,7 +578,8 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
         largest = std::max(largest, cum[i].back());
         check(w2v_dev_set_order(reps[i], shard[i].data(), (int64_t)shard[i].size()), "w2v_dev_set_order");
       }
-      const int64_t rounds = sync_words > 0 ? std::max<int64_t>(1, (largest + sync_words - 1) / sync_words) : 1;
+      const int64_t rounds = sync_words > 0 ? std::max<int64_t>(1, (largest + sync_words - 1) / sync_words)
+                                            : std::max<int64_t>(1, std::min<int64_t>(auto_rounds, largest));
       for (int64_t r = 0; r < rounds; ++r) {
         int64_t words = 0;
         for (size_t i = 0; i < R; ++i) {

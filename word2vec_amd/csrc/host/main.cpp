@@ -41,9 +41,11 @@ void usage() {
                "  -replay <0|1>         reference-exact deterministic RNG replay on one wavefront\n"
                "  -shared-negatives <0|1> skip-gram NS as the shared-negatives minibatch on the matrix cores\n"
                "  -gpus <int>           data-parallel replicas on devices gpu .. gpu+n-1, averaged with RCCL (default 1)\n"
-               "  -sync-words <int>     average the replicas every this many words of a shard (default 0: per epoch)\n"
+               "  -sync-words <int>     exchange the replicas' updates every this many words of a shard\n"
+               "                        (default 0: 64 exchanges per epoch)\n"
                "  -overlap <0|1>        overlap the averaging with the next round's training (default 1)\n"
-               "  -replica-mode <sum|average|row_average|adaptive> how the replicas' updates combine (default average)\n"
+               "  -replica-mode <auto|sum|average|row_average|adaptive> how the replicas' updates combine\n"
+               "                        (default auto: sum for 2 replicas, average for more)\n"
                "  -gpu-ingest <0|1>     count and map the corpus on the GPU (default 0: host threads)\n\n"
                "example: ./word2vec -train text8 -output vec.txt -size 300 -window 5 -subsample 1e-4 "
                "-negative 5 -model sg -train_method ns -iter 3\n";
@@ -76,7 +78,7 @@ int main(int argc, char** argv) {
   const bool cbow_mean = true;
   int binary = 0, gpu = 0, replay = 0, shared = 0, gpus = 1, overlap = 1, gpu_ingest = 0;
   long long sync_words = 0;
-  std::string replica_mode = "average";
+  std::string replica_mode = "auto";
   int i;
   if ((i = find_flag("-size", argc, argv)) > 0) word_dim = std::atoi(argv[i + 1]);
   if ((i = find_flag("-train", argc, argv)) > 0) input_file = argv[i + 1];
@@ -111,8 +113,8 @@ int main(int argc, char** argv) {
     for (int k = 0; k < 4; ++k)
       if (replica_mode == names[k]) replica_mode_id = k;  // W2V_GROUP_SUM .. W2V_GROUP_ADAPTIVE
   }
-  if (replica_mode_id < 0) {
-    std::cout << "Please set -replica-mode to sum, average, row_average or adaptive!" << std::endl;
+  if (replica_mode_id < 0 && replica_mode != "auto") {
+    std::cout << "Please set -replica-mode to auto, sum, average, row_average or adaptive!" << std::endl;
     return 1;
   }
 

@@ -15,7 +15,7 @@ from .host import HOST_LIB
 
 _lib = None
 # Word2Vec::replica_mode values (include/w2v_dev.h W2V_GROUP_*)
-REPLICA_MODES = {"sum": 0, "average": 1, "row_average": 2, "adaptive": 3}
+REPLICA_MODES = {"auto": -1, "sum": 0, "average": 1, "row_average": 2, "adaptive": 3}
 
 
 def _load():
@@ -95,7 +95,7 @@ class Word2Vec:
                  train_method="hs", model="cbow", gpu_device=0, replay_rng=False, verbose=False, hot_rows=-2,
                  private_rows=-1, flush_centers=0, private_average=8.0, max_waves=0, shared_negatives=False,
                  context_rows=-1, context_flush=0, gpu_devices=None, sync_words=0, overlap_average=True,
-                 replica_mode="average", gpu_ingest=False, ingest_chunk_bytes=0, checkpoint_path=""):
+                 replica_mode="auto", gpu_ingest=False, ingest_chunk_bytes=0, checkpoint_path=""):
         self.L = _load()
         self.word_dim = word_dim
         self.h = self.L.w2v_model_new(iter, window, min_count, table_size, word_dim, negative, subsample_threshold,

@@ -5,13 +5,20 @@ The reference parallelises only with OpenMP threads sharing one model
 (torchrun), gives each rank a contiguous shard of the sentences and a full
 model replica in its HBM, trains the shard with the Hogwild kernels, and at
 the end of every round (every `sync_every` sentences of the largest shard, the
-same round count on every rank) averages the replicas.
+same round count on every rank) exchanges what the replicas learned.
 
 The exchange is native: `NativeAverager` wraps the C-ABI's RCCL group
 (include/w2v_dev.h w2v_group_*: the replicas' updates since the last exchange
-summed with one ncclAllReduce per matrix over xGMI and averaged per row over
-the replicas that changed it, optionally overlapped with the next round's
-training). `TorchAverager` (model averaging
+summed with one ncclAllReduce per matrix over xGMI, then combined per `mode`:
+"sum" (every update once, as one shared model), "average" (model averaging:
+the mean), "row_average" (per row, the mean over the replicas that changed
+it), "adaptive", or the per-row divisors of set_split / set_saturation;
+optionally overlapped with the next round's training). The constructor's
+default is "sum" with overlap off (the primitive, as the tests drive it);
+bench.py and Word2Vec::replica_mode pick "auto": sum for two replicas,
+average for more (summing R >= 3 replicas diverges on the frequent rows;
+measured table in DESIGN.md §6), with the exchange overlapped.
+`TorchAverager` (model averaging
 over torch.distributed) is what the CPU tests run on the gloo backend to
 exercise the round logic, which is the same object code.
 
