@@ -1202,10 +1202,18 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     // every slot run faster still with the same scores: of 8 slots, 8 private
     // rows +4 % over 4 + 4 staging; of 10 slots (single transpose buffer), 10
     // private +3.8 % over 4 (profiles/r02z_priv.log, r02z_c5_slots10.log,
-    // r02z_sn_quality_probe*.log).
+    // r02z_sn_quality_probe*.log). Those measurements are at negative 5. At
+    // configs[4]'s own negative 15 every center draws three times as many of
+    // the hottest C rows, a workgroup's 1024-center pending delta of them is
+    // three times as stale, and the averaged flush costs the text8-like gate 8
+    // similarity points (90.7-91.6 / 62.8-65.1 with 2-32 averaged contributions
+    // against 98.1 / 72.2 with no private rows, the sequential minibatch
+    // scoring 98.3 / 69.7: profiles/r03q_c5_*.log), so the automatic setting
+    // keeps no private rows above negative 5 (their slots stage atomic rows).
     {
       const int64_t slots = std::min<int64_t>(32, w2v::kSnPrivBytes / (h->pitch * (int64_t)sizeof(float)));
-      const int64_t want = h->private_rows < 0 ? std::min<int64_t>(10, slots) : h->private_rows;
+      const int64_t want = h->private_rows < 0 ? (h->cfg.negative <= 5 ? std::min<int64_t>(10, slots) : 0)
+                                               : h->private_rows;
       a.priv_n = h->sched == W2V_SCHED_PARALLEL ? (int32_t)std::min<int64_t>({slots, h->V, want}) : 0;
     }
     a.flush_every = h->flush_centers > 0 ? h->flush_centers : 1024;
