@@ -447,17 +447,23 @@ def cpu_baseline(args, counts_v, ids_h, soff_h, neg, mode):
     oracle/w2v_oracle.cpp with its per-call hash map / set, static schedule,
     shared alpha) compiled with the reference's own flags (main.cpp:2: -Ofast
     -march=native -funroll-loops -fopenmp, built on this host), timed on ALL
-    the host cores this process may run on (len(os.sched_getaffinity(0)), as
-    SURVEY.md §8(d) asks: OMP_NUM_THREADS = nproc; the environment's
-    OMP_NUM_THREADS is reported, not used) over a bounded prefix of the same
+    the host cores this process may use (OMP_NUM_THREADS =
+    nproc): the CPUs of its affinity set (len(os.sched_getaffinity(0))),
+    capped by the cgroup's CPU quota where there is one — on the GPU box the
+    affinity set is the whole 256-CPU machine but the quota is 16 CPUs, and
+    256 threads on 16 CPUs' time measure the scheduler, not the reference
+    (r03z: 0.08 M words/s, below one thread's 0.16 M); the environment's
+    OMP_NUM_THREADS is reported, not used. Over a bounded prefix of the same
     shard (same params):
-      value                     all affinity threads, ONE shared mt19937 (the reference's data race)
+      value                     those threads, ONE shared mt19937 (the reference's data race)
       per_thread_rng_value      the same, one mt19937 per thread
       single_thread_value       one thread"""
     import oracle
 
     topo = host_topology()
     threads = topo["affinity_cpus"]
+    if topo["cgroup_cpu_quota"]:
+        threads = max(1, min(threads, int(-(-topo["cgroup_cpu_quota"] // 1))))
     path, flags = oracle.build_fast()
     native = oracle.BaselineLib(path)
 
@@ -497,7 +503,8 @@ def cpu_baseline(args, counts_v, ids_h, soff_h, neg, mode):
             "cpu": cpu_model(), **topo, "flags": flags,
             "sample": f"{n} sentences ({w} in-vocab tokens) of the same shard, {dt:.1f}s: the reference's OpenMP "
                       f"loop restated (oracle/w2v_oracle.cpp orc_train_omp_shared), built with {flags}, "
-                      f"{threads} threads (every CPU of the process's affinity set) sharing one mt19937 as the "
+                      f"{threads} threads (the process's usable CPUs: its affinity set, {topo['affinity_cpus']} "
+                      f"CPUs, capped by the cgroup quota, {topo['cgroup_cpu_quota']}) sharing one mt19937 as the "
                       f"reference does; per_thread_rng_value: {n_p} sentences, {dtp:.1f}s, one mt19937 per "
                       f"thread; single_thread_value: {n1} sentences, {dt1:.1f}s"
                       + ("; the reference's per-pair update: the shared-negatives minibatch has no reference CPU path"

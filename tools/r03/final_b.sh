@@ -21,4 +21,7 @@ for pr in 10 -1 10 -1; do
   timeout -k 10 200 python bench.py --config c5 --steps 3 --warmup 1 --cpu-seconds 0 --private-rows $pr > gpurun_out/${TAG}_c5_pr$pr.json 2> gpurun_out/${TAG}_c5_pr$pr.err || stop c5_pr $?
   echo "c5 private_rows=$pr $(python -c "import json;d=json.load(open('gpurun_out/${TAG}_c5_pr$pr.json'));print(round(d['value']/1e6,2),d['roofline']['frac'],d['ms_per_step'],d['config']['policy_used'])")"
 done
+# the headline line again with the CPU baseline on the usable cores (affinity capped by the cgroup quota)
+timeout -k 10 400 python -u bench.py > gpurun_out/${TAG}_bench_c3.json 2> gpurun_out/${TAG}_bench_c3.err || stop bench_c3 $?
+cat gpurun_out/${TAG}_bench_c3.json
 echo PHASE_DONE
