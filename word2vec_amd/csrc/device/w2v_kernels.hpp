@@ -277,19 +277,39 @@ __device__ __forceinline__ PrivRows ctx_rows(const TrainArgs& a, float* lds) {
 #ifndef W2V_ROW_GUARDS  // timing experiments only (tools/r03): 1 = the per-element guards of round 2
 #define W2V_ROW_GUARDS 0
 #endif
+// W2V_ROW_BOUNDED: the row's last vector (the only one holding padding) goes
+// through a buffer resource whose range is the row's d floats: a lane past it
+// loads 0 and stores nothing WITHOUT an exec mask and without moving the
+// padding's bytes (d 100: 112 of a row's 512 B). Same values as the unbounded
+// form (the padding is zero).
+#ifndef W2V_ROW_BOUNDED
+#define W2V_ROW_BOUNDED 0
+#endif
+constexpr int kBufSc1 = 16;  // buffer cache-policy bit sc1: device scope (bypasses the CU's L1)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const float* base, int d) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, d * 4, 0x00020000);
+}
+
 template <int NV>
 __device__ __forceinline__ void load_row(const float* M, int64_t row, int64_t pitch, int d, int lane, bool fresh,
                                          float (&r)[NV]) {
   const float* p = M + row * pitch + lane;
+  constexpr int NU = W2V_ROW_BOUNDED ? NV - 1 : NV;  // vectors loaded unbounded
   if (fresh) {  // agent-scope relaxed loads: global_load_dword sc1, bypass the CU's L1
 #pragma unroll
-    for (int v = 0; v < NV; ++v)
+    for (int v = 0; v < NU; ++v)
       r[v] = (!W2V_ROW_GUARDS || lane + kWave * v < d)
                  ? __hip_atomic_load(p + kWave * v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                  : 0.f;
   } else {
 #pragma unroll
-    for (int v = 0; v < NV; ++v) r[v] = (!W2V_ROW_GUARDS || lane + kWave * v < d) ? p[kWave * v] : 0.f;
+    for (int v = 0; v < NU; ++v) r[v] = (!W2V_ROW_GUARDS || lane + kWave * v < d) ? p[kWave * v] : 0.f;
+  }
+  if (W2V_ROW_BOUNDED) {
+    const uint32_t off = (uint32_t)(lane + kWave * (NV - 1)) * 4u;
+    const __amdgpu_buffer_rsrc_t rs = row_rsrc(M + row * pitch, d);
+    r[NV - 1] = __uint_as_float(fresh ? __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, kBufSc1)
+                                      : __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
   }
 }
 
@@ -297,9 +317,13 @@ template <int NV>
 __device__ __forceinline__ void store_row(float* M, int64_t row, int64_t pitch, int d, int lane,
                                           const float (&r)[NV]) {
   float* p = M + row * pitch + lane;
+  constexpr int NU = W2V_ROW_BOUNDED ? NV - 1 : NV;
 #pragma unroll
-  for (int v = 0; v < NV; ++v)
+  for (int v = 0; v < NU; ++v)
     if (!W2V_ROW_GUARDS || lane + kWave * v < d) p[kWave * v] = r[v];
+  if (W2V_ROW_BOUNDED)
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r[NV - 1]), row_rsrc(M + row * pitch, d),
+                                          (uint32_t)(lane + kWave * (NV - 1)) * 4u, 0, 0);
 }
 
 // row += delta, memory-side (no-return global_atomic_add_f32, 256 contiguous B
