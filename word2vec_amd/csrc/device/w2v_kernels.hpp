@@ -281,7 +281,9 @@ __device__ __forceinline__ PrivRows ctx_rows(const TrainArgs& a, float* lds) {
 // through a buffer resource whose range is the row's d floats: a lane past it
 // loads 0 and stores nothing WITHOUT an exec mask and without moving the
 // padding's bytes (d 100: 112 of a row's 512 B). Same values as the unbounded
-// form (the padding is zero).
+// form (the padding is zero). Measured (profiles/r03t_bounded_ab.log; parity
+// green): 0.2-0.3 % slower on configs[0]-[2] — the padding shares its 128-B
+// line with the row's last valid floats, so no line is saved. Off.
 #ifndef W2V_ROW_BOUNDED
 #define W2V_ROW_BOUNDED 0
 #endif
