@@ -220,8 +220,8 @@ int w2v_dev_reset_stats(w2v_dev* h);
  *    the default) = chosen per launch from the corpus statistics: the rows
  *    and nodes whose expected updates in flight (wavefronts x expected
  *    updates per center) reach the thresholds of w2v_dev_set_hot_auto
- *    (W / C rows: by the vocabulary by default, 4 when a row's average
- *    updates in flight waves x (window + 1) / V is <= 1, else 1; nodes: 1);
+ *    (W / C rows: by the vocabulary by default, 2 when a row's average
+ *    updates in flight waves x (window + 1) / V is <= 0.1, else 1; nodes: 1);
  *    -1 = every row, 0 = none,
  *    k > 0 = the k most frequent;
  *  - the rest: plain read-modify-write (an update racing another on the same

@@ -149,6 +149,8 @@ def train(args, R, rounds, gmode, overlap, seed, data, dev):
         t.set_train_words(max(1, int(args.raw_tokens) // R))
         t.set_rng(N.W2V_RNG_PHILOX, (seed << 32) | 0x5EED)
         t.set_schedule(N.W2V_SCHED_PARALLEL)
+        if args.hot_tau > 0:  # automatic hot rows at this threshold (0 = the library's rule by vocabulary)
+            t.set_hot_auto(args.hot_tau, 1.0)
         if args.max_waves > 0:  # the same total concurrency for every R
             t.set_max_waves(max(1, args.max_waves // R))
         reps.append(t)
@@ -217,6 +219,7 @@ def main():
     ap.add_argument("--planted-frac", type=float, default=0.10)
     ap.add_argument("--hot-rows", type=int, default=0, help="hot rows exchanged between the full exchanges (0 = none)")
     ap.add_argument("--hot-rounds", type=int, default=0, help="hot-row exchanges per epoch")
+    ap.add_argument("--hot-tau", type=float, default=0.0, help="automatic hot-row threshold (0 = by vocabulary)")
     ap.add_argument("--lr-scale", type=float, default=1.0, help="init_alpha x this for R > 1 (linear scaling rule)")
     ap.add_argument("--max-waves", type=int, default=0, help="cap the waves of all R replicas together (each gets max_waves // R; 0 = full chip each)")
     args = ap.parse_args()
@@ -230,7 +233,7 @@ def main():
     print(json.dumps({"corpus_tokens": int(args.raw_tokens), "in_vocab": int(ids.size), "V": int(counts.size),
                       "sentences": int(n_sent), "gen_s": round(time.time() - t0, 1), "mode": args.mode,
                       "dim": args.dim, "iters": args.iters, "planted_frac": args.planted_frac,
-                      "max_waves": args.max_waves, "lr_scale": args.lr_scale}), flush=True)
+                      "max_waves": args.max_waves, "lr_scale": args.lr_scale, "hot_tau": args.hot_tau}), flush=True)
     data = (ids, soff, counts, words, args.mode)
     for seed in [int(s) for s in args.seeds.split(",")]:
         hr = args.hot_rows

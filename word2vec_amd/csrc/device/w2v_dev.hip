@@ -952,17 +952,21 @@ static double private_rate_for(const w2v_dev* h, int64_t count) {
 // read-modify-write; profiles/r02c_*). Returns {W / C rows, nodes}.
 // The W / C threshold when hot_tau_rows is 0 (the default): by the average
 // number of a row's updates in flight, rho = waves x (window + 1) / V. A large
-// vocabulary (rho <= 0.1: configs[2] 0.033) takes 4: the rows between 1 and 4
-// expected updates in flight race rarely enough for plain read-modify-write,
-// and 1738 -> 435 atomic rows run configs[2] 2-11 % faster, box to box
-// (profiles/r03a_hot_tau.log, r02z_hot_tau_probe.log). A smaller one keeps 1:
+// vocabulary (rho <= 0.1: configs[2] 0.066) takes 2: 1738 -> 867 atomic rows,
+// configs[2] +1.1 % (profiles/r03w_*). Threshold 4 (435 rows, +2-11 % box to
+// box: r03a_hot_tau.log, r02z_hot_tau_probe.log) was the round-3 default
+// until a planted corpus at configs[2]'s own scale (d300, V 717K, rho 0.07,
+// 3 seeds, profiles/r03w_hot_tau_headline_scale_3seeds.log) measured what it
+// costs: analogy 99.9 / 99.5 / 93.0 / 94.9 at threshold 1 / 2 / 4 / 16 —
+// the rows between 2 and 4 updates in flight do lose updates that matter.
+// A smaller vocabulary keeps 1:
 // configs[0] (rho 0.2) gains 1-2 %, the text8-like gate corpus (rho 0.5) lost
 // up to 2.6 similarity points at 4 (one seed of three at -0.9 vs the oracle,
 // r03a), and at 4 the planted SG-HS run (V = 3.4K, rho 14) collapsed: its
 // center rows fell to plain read-modify-write (analogy 6 vs 89,
 // profiles/r02c_*). The shared-negatives kernel keeps 1 (its floor of 1000
 // atomic rows decides there).
-constexpr double kHotTauLargeV = 4.0, kHotTauSmallV = 1.0, kHotRhoLargeV = 0.1;
+constexpr double kHotTauLargeV = 2.0, kHotTauSmallV = 1.0, kHotRhoLargeV = 0.1;
 static double hot_tau_for(const w2v_dev* h, double waves, bool shared) {
   if (h->hot_tau_rows > 0.0) return h->hot_tau_rows;
   if (shared || h->V <= 0) return kHotTauSmallV;
