@@ -38,12 +38,20 @@ MODES = {
     "sg_sn": dict(cbow=False, hs=False, shared=True),
 }
 MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X dense f32-input MFMA (MI355X_MICROARCH.md)
+# configs[3] (10 B tokens on 8 GPUs) under Word2Vec::sync_words = 0 (the class's
+# automatic cadence, 64 exchanges per epoch: Word2Vec.cpp kAutoReplicaRounds):
+# one exchange per 10e9 / 8 / 64 words of a replica's shard. bench.py --gpus N
+# is configs[3]'s per-GPU step, so it exchanges at that cadence (3 exchanges per
+# 50 M-token step) — what the product runs on that workload.
+CONFIG3_SYNC_WORDS = 10_000_000_000 // 8 // 64
 
 # BASELINE.json configs on this bench's synthetic Zipf corpora (text8 and the
 # 1B-Word corpus are not available offline): --config cN sets these fields.
 CONFIGS = {
-    "c1": dict(mode="sg_ns", dim=100, negative=5, vocab=250_000, tokens=17_000_000),    # text8-shaped SGNS d100
-    "c2": dict(mode="cbow_hs", dim=200, negative=0, vocab=250_000, tokens=17_000_000),  # text8-shaped CBOW-HS d200
+    # text8-shaped (configs[0] / [1]): 17 M tokens, p(r) ~ (r + 4)^-1.30 over 350 K ranks gives V ~ 71 K at
+    # min_count 5, ~254 K types, the most frequent word 6 % of tokens (text8: 71,290 / 253,854 / 6.2 %)
+    "c1": dict(mode="sg_ns", dim=100, negative=5, vocab=350_000, zipf_s=1.30, zipf_q=4.0, tokens=17_000_000),
+    "c2": dict(mode="cbow_hs", dim=200, negative=0, vocab=350_000, zipf_s=1.30, zipf_q=4.0, tokens=17_000_000),
     "c3": dict(mode="sg_ns", dim=300, negative=5, vocab=1_000_000, tokens=50_000_000),  # 1B-Word stand-in (default)
     "c4": dict(mode="sg_ns", dim=300, negative=5, vocab=1_000_000, tokens=50_000_000),  # per GPU of the N-GPU run
     "c5": dict(mode="sg_sn", dim=512, negative=15, vocab=1_000_000, tokens=50_000_000),  # shared-negatives MFMA
@@ -64,7 +72,8 @@ def parse():
     ap.add_argument("--vocab", type=int, default=1_000_000, help="Zipf rank range (V before min_count)")
     ap.add_argument("--tokens", type=int, default=50_000_000, help="raw tokens per GPU per step")
     ap.add_argument("--sent-len", type=int, default=1000)
-    ap.add_argument("--zipf-s", type=float, default=1.0, help="corpus law p(rank) ~ rank^-s (1 = Zipf)")
+    ap.add_argument("--zipf-s", type=float, default=1.0, help="corpus law p(rank) ~ (rank + q)^-s (1 = Zipf)")
+    ap.add_argument("--zipf-q", type=float, default=0.0, help="Zipf-Mandelbrot offset q of the corpus law")
     ap.add_argument("--subsample", type=float, default=1e-4)
     ap.add_argument("--min-count", type=int, default=5)
     ap.add_argument("--table-size", type=int, default=100_000_000)
@@ -92,7 +101,10 @@ def parse():
     ap.add_argument("--own-model", action="store_true",
                     help="N=1 only: let the library allocate the matrices instead of torch")
     ap.add_argument("--sync-every", type=int, default=0,
-                    help="average the replicas every this many sentences of a shard (0 = once per step)")
+                    help="N>1: exchange every this many sentences of a shard (0 = by --sync-words)")
+    ap.add_argument("--sync-words", type=int, default=CONFIG3_SYNC_WORDS,
+                    help="N>1: exchange every this many in-vocab words of a shard (default: the class's automatic "
+                         "cadence on configs[3], 64 exchanges per epoch of a 1.25 B-token shard)")
     ap.add_argument("--replica-mode", default="auto", choices=["auto", "sum", "average", "row_average", "adaptive"],
                     help="N>1: how the replicas' updates combine (auto: sum for 2 ranks, average for more, "
                          "as Word2Vec::replica_mode; DESIGN.md §6)")
@@ -147,7 +159,7 @@ def main():
     n_tok = n_sent * args.sent_len
     g = torch.Generator(device=dev)
     g.manual_seed(args.seed * 1000 + rank)
-    p = torch.arange(1, args.vocab + 1, device=dev, dtype=torch.float64).pow_(-args.zipf_s)
+    p = torch.arange(1, args.vocab + 1, device=dev, dtype=torch.float64).add_(args.zipf_q).pow_(-args.zipf_s)
     cdf = torch.cumsum(p, 0)
     cdf /= cdf[-1].clone()
     ranks = torch.empty(n_tok, dtype=torch.int64, device=dev)
@@ -247,7 +259,10 @@ def main():
     else:  # N = 1 (no-op) or the one-GPU rehearsal (ranks share cuda:0: RCCL needs one rank per GPU)
         averager = TorchAverager(mats, world)
     rmode_used = (args.replica_mode if args.replica_mode != "auto" else ("sum" if world <= 2 else "average"))
-    rounds = n_rounds(n_sent * world, world, args.sync_every)
+    if args.sync_every > 0 or world == 1:
+        rounds = n_rounds(n_sent * world, world, args.sync_every)
+    else:  # every rank's shard has ~ the same words: the same round count everywhere
+        rounds = max(1, -(-int(ids_h.size) // max(1, args.sync_words)))
     order_dev = torch.arange(n_sent, dtype=torch.int64, device=dev)  # this rank's shard, in order
     round_words = global_round_words(local_round_words(soff_h, range(n_sent), rounds), world)
     progress = 0
@@ -302,11 +317,14 @@ def main():
     bytes_per_launch = (4 * d * row_moves + 4 * delta["draws"]) / n_launch
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
     achieved = bytes_per_launch / avg_kernel_s / 1e9
-    traffic, traffic_src = pmc_traffic(args)
+    traffic, traffic_src, traffic_ms = pmc_traffic(args)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": "train_epoch_kernel", "avg_launch_ms": round(avg_kernel_s * 1e3, 3),
-                "algorithmic_bytes_per_launch": int(bytes_per_launch)}
+                "algorithmic_bytes_per_launch": int(bytes_per_launch),
+                # the rocprofv3 average of the profile `traffic` comes from (another lease's box: MI355X
+                # boxes differ by up to ~10 %), next to this run's own HIP-event average
+                "profile_box_ms": traffic_ms}
     if mode.get("shared"):
         # MFMA work issued per kept center: three 16 x 16 x pitch f32 GEMMs (L, dW, dC)
         flops = 3 * 2 * 16 * 16 * pitch * delta["centers"] / n_launch
@@ -347,7 +365,8 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": f"{args.mode} neg{neg} d{d} w{args.window} subsample {args.subsample} min_count "
-                            f"{args.min_count}; synthetic Zipf(s={args.zipf_s:g}) over {args.vocab} ranks "
+                            f"{args.min_count}; synthetic Zipf(s={args.zipf_s:g}"
+                            + (f", q={args.zipf_q:g}" if args.zipf_q else "") + f") over {args.vocab} ranks "
                             + {"c1": "standing in for text8 (configs[0]'s workload)",
                                "c2": "standing in for text8 (configs[1])",
                                "c4": "per GPU of configs[3]",
@@ -355,13 +374,15 @@ def main():
                                    args.config, "(configs[4], shared-negatives minibatch)" if mode.get("shared") else
                                    "standing in for 1B-Word (configs[2])") + f"; {args.sent_len}-token sentences",
                 "baseline_config": args.config or ("c5" if mode.get("shared") else "c3"),
+                "traffic_key": traffic_key(args),
                 "tokens_per_gpu_per_step": n_tok,
                 "in_vocab_tokens_per_gpu_per_step": int(ids_h.size),
                 "vocab_size": V,
                 "global_batch": n_tok * world,
                 "parallelism": (f"dp{world}: full replica per GPU, corpus shard per GPU, RCCL all-reduce "
                                 f"of the updates, {rmode_used} (w2v_group, "
-                                f"{'overlapped' if not args.no_overlap else 'blocking'}) x{rounds} per step"
+                                f"{'overlapped' if not args.no_overlap else 'blocking'}) x{rounds} per step "
+                                f"(every {int(ids_h.size) // rounds} words of a shard)"
                                 if world > 1 else "dp1"),
                 "hot_rows": args.hot_rows,
                 "private_rows": args.private_rows,
@@ -394,14 +415,22 @@ def pmc_traffic(args):
     it came from: (bytes, source) or (None, None)."""
     f = ROOT / "profiles" / "pmc_traffic.json"
     if not f.exists():
-        return None, None
+        return None, None, None
     try:
-        rec = json.loads(f.read_text()).get(f"{args.mode}_d{args.dim}_n{args.tokens}")
+        rec = json.loads(f.read_text()).get(traffic_key(args))
     except (OSError, ValueError):
-        return None, None
+        return None, None, None
     if isinstance(rec, dict):
-        return rec.get("traffic"), rec.get("source")
-    return None, None
+        return rec.get("traffic"), rec.get("source"), rec.get("avg_duration_ms_rocprof")
+    return None, None, None
+
+
+def traffic_key(args) -> str:
+    """profiles/pmc_traffic.json key of this workload (tools/pmc_summary.py)."""
+    k = f"{args.mode}_d{args.dim}_n{args.tokens}"
+    if args.zipf_s != 1.0 or args.zipf_q != 0.0 or args.vocab != 1_000_000:
+        k += f"_v{args.vocab}_s{args.zipf_s:g}_q{args.zipf_q:g}"
+    return k
 
 
 def cpu_model() -> str:

@@ -181,6 +181,7 @@ class Word2Vec {
   bool resume_ = false;             // load_checkpoint: the next train continues (no init_weights)
   int64_t start_words_ = 0;         //   ... from this current_words
   int64_t resume_epochs_ = 0;       //   ... after this many epochs of the schedule
+  int64_t resume_iter_ = 0;         //   ... of a schedule of this many epochs (compared with iter at train time)
   uint64_t resume_key_ = 0;         //   ... with this Philox key
   int64_t epochs_done_ = 0;         // epochs of the last train call's schedule completed
   uint64_t key_ = 0;                // Philox key of the last train call
@@ -190,6 +191,7 @@ class Word2Vec {
   void checkpoint_epoch(int64_t cw, int64_t epochs_done, uint64_t key);
   std::string generator_state() const;
   void restore_generator(const std::string& state);
+  bool continues_schedule() const;
   w2v_ingest* ingest_ = nullptr;    // gpu_ingest: the counted file ...
   std::string ingest_key_;          //   ... (path + format)
   std::vector<std::string> ingest_words_;  // its distinct words, in order of first occurrence

@@ -83,21 +83,24 @@ def errs(a, b):
     return rel_err(a, b), elem_rel_err(a, b)
 
 
-def check_parity(got, want, init, norm_tol, elem_tol, tag=""):
+def check_parity(got, want, init, norm_tol, elem_tol, tag="", ulp_matrices=(), overrides=None):
     """Assert both bounds on every matrix's update (got - init vs want - init):
     norm-wise rel_err < norm_tol AND per-element elem_rel_err < elem_tol; a
-    matrix the oracle left untouched must come back bit-identical. A matrix
-    whose update is far below its values (CBOW-NS's W in a single sentence:
-    C starts at zero, so W moves by ~1e-6 of its magnitude) is instead held to
-    the fp32 rounding of its stored values: max |got - want| <= 2 ulp of max
-    |want| (one rounding of `row + g * x` differing in the last bit, from a g
-    that differs in the 7th digit, is 1 ulp of the row, which relative to such
-    an update exceeds 1e-5). Each measurement is printed and, with
-    W2V_PARITY_LOG=<file>, appended to it as a JSON line (the measured errors
-    the bounds in the tests come from)."""
+    matrix the oracle left untouched must come back bit-identical.
+    `overrides` = {matrix index: (norm_tol, elem_tol)} gives a matrix its own
+    measured bounds. A matrix listed in `ulp_matrices` — only CBOW-NS's W in a
+    single update (test_replay_single_sentence): C starts at zero, so W moves
+    by ~1e-6 of its magnitude — may instead meet the fp32 rounding of its
+    stored values: max |got - want| <= 2 ulp of max |want| (one rounding of
+    `row + g * x` differing in the last bit, from a g that differs in the 7th
+    digit, is 1 ulp of the row, which relative to such an update exceeds
+    1e-5); when that clause is what passes, it is printed and logged. Each
+    measurement is printed and, with W2V_PARITY_LOG=<file>, appended to it as a
+    JSON line (the measured errors the bounds in the tests come from)."""
     import json
     import os
 
+    overrides = overrides or {}
     out = []
     for k, (g, w, i) in enumerate(zip(got, want, init)):
         if w is None:
@@ -109,14 +112,17 @@ def check_parity(got, want, init, norm_tol, elem_tol, tag=""):
         en, ee = errs(np.asarray(g, np.float64) - i, dw)
         abs_err = float(np.abs(np.asarray(g, np.float64) - np.asarray(w, np.float64)).max())
         ulps = abs_err / float(np.spacing(np.float32(np.abs(w).max())))
-        out.append((k, en, ee, ulps))
-        print(f"{tag} matrix {k}: rel_err {en:.2e} elem_rel_err {ee:.2e} max_abs_err {ulps:.2f} ulp")
+        nt, et = overrides.get(k, (norm_tol, elem_tol))
+        by_ulp = en >= nt and k in ulp_matrices and ulps <= 2.0
+        out.append((k, en, ee, ulps, nt, et, by_ulp))
+        print(f"{tag} matrix {k}: rel_err {en:.2e} elem_rel_err {ee:.2e} max_abs_err {ulps:.2f} ulp"
+              + (f" (norm-wise above {nt:g}: passes on the 2-ulp clause)" if by_ulp else ""))
         path = os.environ.get("W2V_PARITY_LOG")
         if path:
             with open(path, "a") as f:
                 f.write(json.dumps({"tag": tag, "matrix": k, "rel_err": en, "elem_rel_err": ee, "ulps": ulps,
-                                    "norm_tol": norm_tol, "elem_tol": elem_tol}) + "\n")
-    for k, en, ee, ulps in out:
-        assert en < norm_tol or ulps <= 2.0, (tag, k, en, norm_tol, ulps)
-        assert ee < elem_tol, (tag, k, ee, elem_tol)
+                                    "norm_tol": nt, "elem_tol": et, "ulp_clause": by_ulp}) + "\n")
+    for k, en, ee, ulps, nt, et, by_ulp in out:
+        assert en < nt or by_ulp, (tag, k, en, nt, ulps)
+        assert ee < et, (tag, k, ee, et)
     return out

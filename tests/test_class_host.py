@@ -217,6 +217,61 @@ def test_checkpoint_load_rejects_bad_shapes(tmp_path):
     np.testing.assert_array_equal(hs.matrix(0), before)
 
 
+def test_checkpoint_version1_loads(tmp_path):
+    """a round-2 (version 1) checkpoint — magic W2VCKPT1, then V,
+    d, vocab hash, current_words, the generator, the matrices; no schedule
+    position — still loads (as a whole-schedule checkpoint); an unknown
+    version is named as such, not as a foreign file."""
+    import struct
+
+    from tests.corpus import zipf_sentences
+    from word2vec_amd.model import Word2Vec
+
+    sents = zipf_sentences(20, 100, 200, seed=4)
+    kw = dict(iter=1, window=5, min_count=2, table_size=10_000, word_dim=12, negative=5, train_method="ns", model="sg")
+    a = Word2Vec(**kw)
+    a.seed(2)
+    a.build_vocab(sents)
+    a.init_weights()
+    a.set_matrix(1, a.matrix(1) + 0.5)
+    a.save_checkpoint(tmp_path / "v2.bin")
+    raw = (tmp_path / "v2.bin").read_bytes()
+    assert raw[:8] == b"W2VCKPT2"
+    head = raw[8:32]  # V, d, vocab hash
+    cw = raw[32:40]
+    q = 8 + 24 + 24 + 8  # past magic, V/d/hash, cw/epochs/iter, key
+    gl = struct.unpack("<q", raw[q:q + 8])[0]
+    gen = raw[q:q + 8 + gl]
+    q += 8 + gl
+    gl2 = struct.unpack("<q", raw[q:q + 8])[0]
+    mats = raw[q + 8 + gl2:]
+    (tmp_path / "v1.bin").write_bytes(b"W2VCKPT1" + head + cw + gen + mats)
+    b = Word2Vec(**kw)
+    b.build_vocab(sents)
+    b.load_checkpoint(tmp_path / "v1.bin")
+    np.testing.assert_array_equal(b.matrix(0), a.matrix(0))
+    np.testing.assert_array_equal(b.matrix(1), a.matrix(1))
+    (tmp_path / "v9.bin").write_bytes(b"W2VCKPT9" + raw[8:])
+    with pytest.raises(RuntimeError, match="version"):
+        b.load_checkpoint(tmp_path / "v9.bin")
+
+
+def test_replica_mode_rejected_early():
+    """replica_mode outside -1 .. W2V_GROUP_ADAPTIVE (e.g. 4 = SPLIT,
+    whose per-row divisors the class does not compute) fails in train() before
+    any replica is created (check_limits), naming the member."""
+    from tests.corpus import zipf_sentences
+    from word2vec_amd.model import Word2Vec
+
+    sents = zipf_sentences(5, 50, 100, seed=1)
+    for bad in (4, 5, -2):
+        w = Word2Vec(iter=1, window=5, min_count=1, table_size=1000, word_dim=16, negative=5, train_method="ns",
+                     model="sg", gpu_devices=[0, 0], replica_mode=bad)
+        w.build_vocab(sents)
+        with pytest.raises(RuntimeError, match="replica_mode"):
+            w.train(sents)
+
+
 def test_hyperparameter_limits_fail_early():
     """The reference accepts any window / negative / word_dim
     (Word2Vec.cpp:254, 285, 335); the GPU kernels' range (w2v_dev_limits) is

@@ -162,6 +162,46 @@ def test_group_hot_rows_exchange(mode, overlap):
         d.close()
 
 
+@pytest.mark.parametrize("overlap", [False, True])
+@pytest.mark.parametrize("mode", ["sg_ns", "cbow_hs"])
+def test_group_hot_then_full_with_training_between(mode, overlap):
+    """an overlapped average(rows=k), then the replicas change
+    (training, here upload_model), then a full average(): the pending hot-row
+    exchange is folded on its own before the full one's deltas are taken. Every
+    change of both rounds must reach both replicas exactly once: after the
+    final finish() each replica holds M0 + sum of all four changes (sum mode).
+    A fold that reset the snapshot to the replica's current rows (P = M) lost
+    the second round's changes of rows [0, k) from the exchange."""
+    o, ds = _pair_of_handles(mode)
+    rng = np.random.default_rng(17)
+    M0 = [None if m is None else rng.standard_normal(m.shape).astype(np.float32) for m in ds[0].download_model()]
+    for d in ds:
+        d.upload_model(*M0)
+    g = NativeAverager(ds, overlap=overlap, mode="sum")
+    k = 40
+    changes = [[None if m is None else (0.1 * rng.standard_normal(m.shape)).astype(np.float32) for m in M0]
+               for _ in range(4)]  # round 1: replica 0, replica 1; round 2: replica 0, replica 1
+    for i, d in enumerate(ds):
+        d.upload_model(*[None if m is None else m + c for m, c in zip(M0, changes[i])])
+    g.average(rows=k)  # in flight (overlap) while the replicas change again
+    for i, d in enumerate(ds):
+        cur = d.download_model()
+        d.upload_model(*[None if m is None else m + c for m, c in zip(cur, changes[2 + i])])
+    g.average()
+    g.finish()
+    g.average()  # round 2's changes travel in the next exchange (overlap: one round late)
+    g.finish()
+    for d in ds:
+        for j, got in enumerate(d.download_model()):
+            if M0[j] is None:
+                continue
+            want = M0[j].astype(np.float64) + sum(c[j].astype(np.float64) for c in changes)
+            np.testing.assert_allclose(got, want, rtol=1e-5, atol=2e-5)
+    g.close()
+    for d in ds:
+        d.close()
+
+
 @pytest.mark.parametrize("gmode", ["sum", "row_average", "average", "adaptive"])
 @pytest.mark.parametrize("overlap", [False, True])
 def test_rccl_exchange_one_rank(overlap, gmode):

@@ -34,6 +34,7 @@ def main(tag, key):
     stats = list(csv.DictReader(open(src / "kt" / "kt_kernel_stats.csv")))
     k = [r for r in stats if "train_" in r["Name"]][0]
     bench = json.loads((src / "kt_bench.json").read_text())
+    key = key or bench["config"]["traffic_key"]
     f_kib = sum(fetch) / len(fetch)
     w_kib = sum(write) / len(write)
     traffic = (2 * f_kib + w_kib) * 1024
@@ -63,4 +64,5 @@ def main(tag, key):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "sg_ns_d300_n50000000")
+    # key: the profiled bench line's own config.traffic_key unless given
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)

@@ -121,7 +121,12 @@ __global__ void replica_delta_kernel(float* M, float* P, float* D, const float* 
   }
 }
 
-// Fold the exchange into the replica: M = M + w A - D, P = M.
+// Fold the exchange into the replica on its own (the pending exchange covers
+// other rows than the one being issued, or none is issued: finish): the same
+// increment x = w A - D goes into M and into the snapshot P. M may already
+// hold updates trained after the exchange was issued (overlap); P = M would
+// absorb them and the next delta M - P would never carry them to the other
+// replicas, while P += x keeps them in M - P.
 __global__ void replica_fold_kernel(float* M, float* P, const float* D, const float* A, const float* cnt, float s,
                                     int64_t pitch, int64_t n_elems) {
   const int64_t n4 = n_elems / 4;
@@ -129,11 +134,14 @@ __global__ void replica_fold_kernel(float* M, float* P, const float* D, const fl
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     const float w = row_weight(cnt, s, i, pitch);
     float4 m = reinterpret_cast<float4*>(M)[i];
+    float4 p = reinterpret_cast<float4*>(P)[i];
     const float4 a = reinterpret_cast<const float4*>(A)[i];
     const float4 d = reinterpret_cast<const float4*>(D)[i];
-    m.x += w * a.x - d.x; m.y += w * a.y - d.y; m.z += w * a.z - d.z; m.w += w * a.w - d.w;
+    const float4 x = make_float4(w * a.x - d.x, w * a.y - d.y, w * a.z - d.z, w * a.w - d.w);
+    m.x += x.x; m.y += x.y; m.z += x.z; m.w += x.w;
+    p.x += x.x; p.y += x.y; p.z += x.z; p.w += x.w;
     reinterpret_cast<float4*>(M)[i] = m;
-    reinterpret_cast<float4*>(P)[i] = m;
+    reinterpret_cast<float4*>(P)[i] = p;
   }
 }
 

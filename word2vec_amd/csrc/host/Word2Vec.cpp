@@ -426,7 +426,7 @@ void Word2Vec::run_epochs(const std::vector<int32_t>& ids, const std::vector<int
   apply_policy(dev_);
   // a checkpoint taken mid-schedule continues that schedule (its counter, key
   // and shuffle stream); anything else starts one: current_words = 0 (:359)
-  const bool cont = resume_ && resume_epochs_ > 0 && resume_epochs_ < iter;
+  const bool cont = continues_schedule();
   const int first = cont ? (int)resume_epochs_ : 0;
   check(w2v_dev_set_progress(dev_, cont ? start_words_ : 0), "w2v_dev_set_progress");
   std::vector<long> sample_idx((size_t)n);
@@ -530,7 +530,7 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
     }
   };
   try {
-    const bool cont = resume_ && resume_epochs_ > 0 && resume_epochs_ < iter;  // as run_epochs
+    const bool cont = continues_schedule();  // as run_epochs
     const int first = cont ? (int)resume_epochs_ : 0;
     const uint64_t key = cont ? resume_key_ : ((uint64_t)generator() << 32) | (uint64_t)generator();
     key_ = key;
@@ -637,6 +637,12 @@ void Word2Vec::check_limits() const {
   if (negative < 0 || negative > mn) bad("negative must be in [0, " + std::to_string(mn) + "] on the GPU path");
   if (shared_negatives && (window > smw || negative > smn))
     bad("shared_negatives needs window <= " + std::to_string(smw) + " and negative <= " + std::to_string(smn));
+  // -1 (auto) or one of the modes w2v_group_set_mode takes; SPLIT / SATURATION
+  // need per-row divisors the class does not compute (checked
+  // before any replica is created)
+  if (replica_mode < -1 || replica_mode > W2V_GROUP_ADAPTIVE)
+    bad("replica_mode must be -1 (auto) or W2V_GROUP_SUM .. W2V_GROUP_ADAPTIVE (0 .. " +
+        std::to_string(W2V_GROUP_ADAPTIVE) + ")");
 }
 
 // Word2Vec.cpp:356-396.
@@ -944,27 +950,43 @@ void Word2Vec::restore_generator(const std::string& state) {
 
 void Word2Vec::save_checkpoint(const std::string& path) { write_checkpoint(path, cur_words_, epochs_done_, key_); }
 
+// Whether the next train call continues a loaded checkpoint's schedule: one
+// taken mid-schedule (0 < epochs done < its iter) of a schedule as long as
+// this object's iter NOW (decided at train time: iter may change after the
+// load).
+bool Word2Vec::continues_schedule() const {
+  return resume_ && resume_epochs_ > 0 && resume_iter_ == iter && resume_epochs_ < iter;
+}
+
 void Word2Vec::load_checkpoint(const std::string& path) {
   std::ifstream in(path, std::ios::binary);
   if (!in) throw std::runtime_error("checkpoint: cannot read " + path);
   char magic[8];
   in.read(magic, 8);
-  if (!in || std::memcmp(magic, kCkptMagic, 8) != 0) throw std::runtime_error("checkpoint: not a word2vec_amd checkpoint");
-  int64_t V = 0, d = 0, cw = 0, ep = 0, it = 0, gl = 0;
+  if (!in || std::memcmp(magic, "W2VCKPT", 7) != 0) throw std::runtime_error("checkpoint: not a word2vec_amd checkpoint");
+  // version 1 (round 2): V, d, vocab hash, current_words, the generator, the
+  // matrices: no schedule position, so it loads as a whole-schedule checkpoint
+  // (the next train starts a new schedule on its weights)
+  const int version = magic[7] == '1' ? 1 : magic[7] == kCkptMagic[7] ? 2 : 0;
+  if (version == 0)
+    throw std::runtime_error(std::string("checkpoint: unknown checkpoint version '") + magic[7] + "' (this build reads 1 and 2)");
+  int64_t V = 0, d = 0, cw = 0, ep = 0, it = 1, gl = 0;
   uint64_t vh = 0, key = 0;
   in.read((char*)&V, 8);
   in.read((char*)&d, 8);
   in.read((char*)&vh, 8);
   in.read((char*)&cw, 8);
-  in.read((char*)&ep, 8);
-  in.read((char*)&it, 8);
-  in.read((char*)&key, 8);
+  if (version >= 2) {
+    in.read((char*)&ep, 8);
+    in.read((char*)&it, 8);
+    in.read((char*)&key, 8);
+  }
   if (!in || V != (int64_t)vocab.size() || d != word_dim || vh != vocab_hash64(vocab))
     throw std::runtime_error("checkpoint: vocabulary or word_dim differs from this object's");
   if (cw < 0 || ep < 0 || it < 1 || ep > it) throw std::runtime_error("checkpoint: bad schedule position");
   std::string gstate[2];  // the generator now, and at the start of the checkpoint's schedule
   std::mt19937 gen;
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < (version >= 2 ? 2 : 1); ++k) {
     in.read((char*)&gl, 8);
     if (!in || gl < 0 || gl > (1 << 20)) throw std::runtime_error("checkpoint: bad generator state");
     gstate[k].assign((size_t)gl, '\0');
@@ -995,8 +1017,9 @@ void Word2Vec::load_checkpoint(const std::string& path) {
   start_words_ = cw;
   epochs_done_ = ep;
   key_ = key;
-  // a mid-schedule checkpoint of the same iter continues it (include/Word2Vec.h)
-  resume_epochs_ = it == iter ? ep : 0;
+  // a mid-schedule checkpoint continues its schedule if iter still matches when train runs
+  resume_epochs_ = ep;
+  resume_iter_ = it;
   resume_key_ = key;
   resume_sched_gen_ = gstate[1];
   sched_gen_ = gstate[1];

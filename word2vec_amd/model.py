@@ -111,7 +111,7 @@ class Word2Vec:
         if gpu_devices:
             devs = np.ascontiguousarray(gpu_devices, np.int32)
             self.L.w2v_model_replicas(self.h, _p(devs), devs.size, int(sync_words), int(bool(overlap_average)))
-            self.L.w2v_model_replica_mode(self.h, REPLICA_MODES[replica_mode])
+            self.L.w2v_model_replica_mode(self.h, REPLICA_MODES.get(replica_mode, replica_mode))
         self.L.w2v_model_set_gpu_ingest(self.h, int(bool(gpu_ingest)), int(ingest_chunk_bytes))
         if checkpoint_path:
             self.set_checkpoint_path(checkpoint_path)
