@@ -115,7 +115,8 @@ class Word2Vec {
   // replicas sharing one GPU), each on a contiguous shard of every epoch's
   // shuffled sentence order, and exchanges their updates (include/w2v_dev.h
   // w2v_group_*: RCCL all-reduce over xGMI) every sync_words in-vocab words of
-  // the largest shard (0 = auto: kAutoReplicaRounds exchanges per epoch),
+  // the largest shard (0 = auto: kAutoReplicaRounds exchanges per epoch when
+  // summing, at most one per kAutoAverageWords words of a shard when averaging),
   // overlapped with the next round's training unless overlap_average is false.
   // replica_mode: a W2V_GROUP_* mode, or -1 = auto: W2V_GROUP_SUM for two
   // replicas, W2V_GROUP_AVERAGE (model averaging) for more — summing R >= 3
@@ -126,6 +127,10 @@ class Word2Vec {
   bool overlap_average = true;
   int replica_mode = -1;
   static const int64_t kAutoReplicaRounds = 64;  // 2 replicas within a point at 32-64 per epoch
+  // sync_words = 0 with averaging (replica_mode average, or auto with > 2
+  // replicas): at most one exchange per this many words of a shard, so each
+  // round's mean spans rows every replica trained
+  static const int64_t kAutoAverageWords = 4000000;
   bool verbose = true;       // progress line per epoch (the reference prints one
                              // every 100 sentences, Word2Vec.cpp:382-386)
   // Train on a corpus that is already token ids (no strings): ids index

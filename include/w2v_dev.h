@@ -96,9 +96,12 @@ const char* w2v_dev_last_error(void); /* thread-local message of the last failur
 const char* w2v_dev_knobs(w2v_dev* h);
 
 /* The kernels' range of the reference's unbounded hyper-parameters
- * (Word2Vec.cpp:254, 285, 335 accept any window / negative): word_dim <= 1024,
- * window <= 127, negative <= 63 (w2v_dev_create returns W2V_ERR_UNSUPPORTED
- * beyond them); the shared-negatives update: window <= 8, negative <= 15.
+ * (Word2Vec.cpp:254, 285, 335 accept any window / negative): word_dim <= 2048,
+ * window <= 65535, negative <= 65535 (w2v_dev_create returns
+ * W2V_ERR_UNSUPPORTED beyond them; negatives past 63 are drawn and
+ * deduplicated 64 at a time, CBOW windows past 127 are walked from the
+ * sentence); the shared-negatives update: window <= 8, negative <= 15 (its
+ * 16 x 16 MFMA tiles hold a window's <= 16 inputs and <= 16 outputs).
  * Callers check these up front (Word2Vec::train, the CLI) to fail before any
  * corpus work, naming the reference's member / flag. Any pointer may be NULL. */
 int w2v_dev_limits(int32_t* max_dim, int32_t* max_window, int32_t* max_negative, int32_t* shared_max_window,
@@ -157,6 +160,12 @@ int w2v_dev_model_layout(w2v_dev* h, float** dW, float** dC, float** dsyn1, int6
 int w2v_dev_upload_corpus(w2v_dev* h, const int32_t* ids, int64_t n_tokens,
                           const int64_t* sent_offsets, int64_t n_sentences,
                           int64_t train_words);
+/* Train on another handle's corpus (same device, same vocab) without a copy:
+ * replicas sharing one GPU (Word2Vec::gpu_devices with a repeated device)
+ * each train their own order slices of ONE resident corpus (configs[3]'s 10 B
+ * tokens are 40 GB: eight copies would not fit one GPU). `src` must outlive
+ * `h`'s training; h keeps its own order buffer and statistics copy. */
+int w2v_dev_share_corpus(w2v_dev* h, w2v_dev* src);
 /* Replay mode: recorded draws in the reference's order (u per token; window
  * shrink per kept token; table positions per NS call) and their start offset
  * per [epoch * n_sentences + sentence]. */

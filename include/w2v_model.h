@@ -95,6 +95,12 @@ int64_t w2v_model_epochs_done(w2v_model* m);
 double w2v_model_epoch_seconds(w2v_model* m, int64_t i);
 int64_t w2v_model_current_words(w2v_model* m);
 int w2v_model_read_vocab(w2v_model* m, const char* path);
+/* Word2Vec::create_huffman_tree / make_table / precalc_sampling
+ * (Word2Vec.h:70-72; Word2Vec.cpp:32-130): the vocabulary products
+ * build_vocab makes (:162-168), for a vocab read with read_vocab. */
+int w2v_model_create_huffman_tree(w2v_model* m);
+int w2v_model_make_table(w2v_model* m);
+int w2v_model_precalc_sampling(w2v_model* m);
 
 #ifdef __cplusplus
 }

@@ -172,7 +172,8 @@ struct PhiloxDraws {
     return (int)(((uint64_t)tok[1] * w) >> 32);
   }
   int table_pos(int slot, int k) {
-    uint32_t ctr[4] = {i, s, ((uint32_t)slot << 8) | (uint32_t)k, epoch}, o[4];
+    // k's low byte next to the slot, its high bits above the epoch (k < 256: the epoch alone)
+    uint32_t ctr[4] = {i, s, ((uint32_t)slot << 8) | ((uint32_t)k & 255u), epoch ^ (((uint32_t)k >> 8) << 20)}, o[4];
     philox4x32_10(ctr, k0, k1, o);
     uint64_t x = ((uint64_t)o[1] << 32) | o[0];
     return (int)(uint64_t)(((unsigned __int128)x * (uint64_t)table_size) >> 64);

@@ -145,3 +145,161 @@ def gpu_trainer(counts, ids, soff, raw, mode, dim, negative, alpha, W0, C0, S0, 
     t.set_schedule(N.W2V_SCHED_PARALLEL)
     t.set_progress(0)
     return t
+
+
+_ROWS, _COLS, _TOPIC, _ROLE = 50, 4, 8, 8  # planted_zipf_ids' grid
+
+
+def _chunks(n_tokens, filler, planted, seed, dev, sent_len, chunk=1 << 26):
+    """The raw ids of the corpus, chunk by chunk (deterministic in `seed`)."""
+    import torch
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    n_sent = n_tokens // sent_len
+    n = n_sent * sent_len
+    E0 = filler
+    T0 = E0 + _ROWS * _COLS
+    R0 = T0 + _ROWS * _TOPIC
+    p = torch.arange(1, filler + 1, device=dev, dtype=torch.float64).reciprocal_()
+    cdf = torch.cumsum(p, 0)
+    cdf /= cdf[-1].clone()
+    si = torch.randint(_ROWS, (n_sent,), generator=g, device=dev)
+    sj = torch.randint(_COLS, (n_sent,), generator=g, device=dev)
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        m = e - s
+        tok = torch.searchsorted(cdf, torch.rand(m, generator=g, device=dev, dtype=torch.float64), right=True)
+        tok.clamp_(max=filler - 1)
+        pos = torch.nonzero(torch.rand(m, generator=g, device=dev) < planted).squeeze(1)
+        k = pos.numel()
+        sent = (pos + s) // sent_len
+        i, j = si[sent], sj[sent]
+        kind = torch.rand(k, generator=g, device=dev)
+        r1 = torch.rand(k, generator=g, device=dev)
+        r2 = torch.rand(k, generator=g, device=dev)
+        ri = torch.randint(_ROWS, (k,), generator=g, device=dev)
+        rj = torch.randint(_COLS, (k,), generator=g, device=dev)
+        rt = torch.randint(_TOPIC, (k,), generator=g, device=dev)
+        rr = torch.randint(_ROLE, (k,), generator=g, device=dev)
+        cross = r1 <= 0.25
+        ei = torch.where(cross & (r2 >= 0.5), ri, i)
+        ej = torch.where(cross & (r2 < 0.5), rj, j)
+        tok[pos] = torch.where(kind < 0.34, E0 + ei * _COLS + ej,
+                               torch.where(kind < 0.67, T0 + i * _TOPIC + rt, R0 + j * _ROLE + rr))
+        yield s, e, tok
+
+
+def planted_zipf_ids_torch(n_tokens, filler, planted, seed, dev, sent_len=1000):
+    """planted_zipf_ids' law (Zipf(s=1) filler, the 50 x 4 planted grid) drawn
+    with torch on `dev` (the GPU: 10 B tokens in seconds; not the same draws as
+    the numpy generator), every rank in vocab (asserted: no OOV, so every
+    sentence keeps its sent_len tokens). Two passes over the same draws (count,
+    then map to vocab indices in count order): (ids int32 [n_sent, sent_len] on
+    the host, counts int64 in vocab order, words, questions, pairs, raw
+    tokens)."""
+    import torch
+
+    n_raw = filler + _ROWS * _COLS + _ROWS * _TOPIC + _COLS * _ROLE
+    counts = torch.zeros(n_raw, dtype=torch.int64, device=dev)
+    n = 0
+    for s, e, tok in _chunks(n_tokens, filler, planted, seed, dev, sent_len):
+        counts += torch.bincount(tok, minlength=n_raw)
+        n = e
+    counts_h = counts.cpu().numpy()
+    order = np.argsort(-counts_h, kind="stable")
+    V = int((counts_h >= 5).sum())
+    assert V == n_raw, f"{n_raw - V} word types below min_count: the study assumes no OOV"
+    remap = np.empty(n_raw, np.int32)
+    remap[order] = np.arange(n_raw, dtype=np.int32)
+    remap_d = torch.from_numpy(remap).to(dev)
+    ids = np.empty(n, np.int32)
+    for s, e, tok in _chunks(n_tokens, filler, planted, seed, dev, sent_len):
+        ids[s:e] = remap_d[tok].cpu().numpy()
+    names = ([f"f{k}" for k in range(filler)] + [f"e{a}_{b}" for a in range(_ROWS) for b in range(_COLS)]
+             + [f"t{a}_{k}" for a in range(_ROWS) for k in range(_TOPIC)]
+             + [f"r{b}_{k}" for b in range(_COLS) for k in range(_ROLE)])
+    words = [names[k] for k in order]
+    rng = np.random.default_rng(seed)
+    qs = [(f"e{a}_{l}", f"e{a}_{b}", f"e{c}_{l}", f"e{c}_{b}") for a in range(_ROWS) for c in range(_ROWS) if a != c
+          for b in range(_COLS) for l in range(_COLS) if b != l]
+    prs = [(f"e{a}_{b}", f"e{c}_{d}", float((a == c) + (b == d))) for a in range(_ROWS) for b in range(_COLS)
+           for c in range(_ROWS) for d in range(_COLS) if (a, b) < (c, d) and rng.random() < 0.05]
+    return ids.reshape(-1, sent_len), counts_h[order].astype(np.int64), words, qs, prs, n
+
+
+def train_replicas(data, R, gmode, rounds, dim=300, negative=5, mode="sg_ns", seed=1, dev=None):
+    """One epoch of `data` (planted_zipf_ids_torch) by R replicas on one
+    device (a same-device w2v_group: every replica a full-concurrency training
+    handle, as on R GPUs; replica r trains the r-th contiguous 1/R of the
+    shuffled sentence order as its own corpus, its counter following the
+    global alpha schedule) exchanging `rounds` times per epoch in `gmode`
+    (auto = Word2Vec::replica_mode's: sum for 2, average for more; overlapped
+    as the class does), or by one replica (R = 1). mode sg_ns or sg_sn (the
+    shared-negatives minibatch). Returns ((analogy, similarity) of W or None
+    if it diverged, train seconds)."""
+    import time
+
+    import torch
+
+    from word2vec_amd import _native as N
+    from word2vec_amd.replicas import NativeAverager
+
+    ids, counts, words, qs, prs, raw = data
+    n_sent, L = ids.shape
+    V, d = counts.size, dim
+    rng = np.random.default_rng(seed)
+    W0 = ((rng.random((V, d), dtype=np.float32) - 0.5) / d).astype(np.float32)
+    C0 = np.zeros((V, d), np.float32)
+    perm = np.random.default_rng(1000 * seed).permutation(n_sent)
+    key = (seed << 32) | 0x5EED
+    reps = []
+    for r in range(R):
+        sh = np.sort(perm[n_sent * r // R: n_sent * (r + 1) // R])  # this replica's sentences (its own corpus)
+        sid = ids.reshape(-1) if R == 1 else np.ascontiguousarray(ids[sh].reshape(-1))
+        soff = np.arange(0, sh.size * L + 1, L, dtype=np.int64)
+        t = gpu_trainer(counts, sid, soff, sh.size * L, "sg_ns", d, negative, 0.025, W0, C0, None, key + r)
+        t.set_train_words(max(1, raw // R))
+        if mode == "sg_sn":
+            t.set_update(N.W2V_UPDATE_SHARED_NEGATIVES)
+        t.set_order(perm.astype(np.int64) if R == 1 else
+                    np.random.default_rng(7 + r).permutation(sh.size).astype(np.int64))
+        reps.append((t, sh.size))
+        del sid
+    del W0, C0
+    g = None
+    if R > 1:
+        gm = ("sum" if R <= 2 else "average") if gmode == "auto" else gmode
+        g = NativeAverager([t for t, _ in reps], overlap=True, mode=gm)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    glob = 0
+    words_per_sent = L
+    rounds = rounds if R > 1 else 1
+    for r in range(rounds):
+        wr = 0
+        for t, m in reps:
+            lo, hi = m * r // rounds, m * (r + 1) // rounds
+            t.set_progress_async(glob // R)
+            if hi > lo:
+                t.train_slice_async(0, lo, hi - lo)
+            wr += (hi - lo) * words_per_sent
+        if g is not None:
+            g.average()
+        glob += wr
+    if g is not None:
+        g.finish()
+    for t, _ in reps:
+        t.synchronize()
+    dt = time.time() - t0
+    st = [t.read_stats() for t, _ in reps]
+    diverged = any(s["nonfinite"] > 0 for s in st)
+    W, _, _ = reps[0][0].download_model()
+    if g is not None:
+        g.close()
+    for t, _ in reps:
+        t.close()
+    if diverged:
+        return None, dt
+    a, s = scores(words, W, qs, prs, dev)
+    return (a, s), dt

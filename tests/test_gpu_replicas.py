@@ -323,3 +323,52 @@ def test_two_replicas_overlapped_full_concurrency_runs():
     sync = sum(len(s) for s in sents) // 2 // 4
     words, E = _train_class(sents, "sg_ns", 2, [0, 0], sync, True, 0)
     assert np.isfinite(E).all() and len(words) > 1000
+
+
+def _class_on_ids(data, vocab_path, gpu_devices, seed=3, dim=100):
+    """Word2Vec (the C++ class) with its defaults on an id corpus: read_vocab +
+    the reference's vocab products, init_weights, train_ids; replicas through
+    gpu_devices (auto mode and cadence, overlapped). Returns (analogy, similarity)."""
+    import torch
+
+    from tests.planted_ids import scores
+    from word2vec_amd.model import Word2Vec
+
+    ids, counts, words, qs, prs, raw = data
+    w = Word2Vec(iter=1, window=5, min_count=5, table_size=100_000_000, word_dim=dim, negative=5,
+                 subsample_threshold=1e-4, init_alpha=0.025, min_alpha=2.5e-6, cbow_mean=True, train_method="ns",
+                 model="sg", gpu_devices=gpu_devices, verbose=False)
+    w.seed(seed)
+    w.read_vocab(vocab_path)
+    w.make_table()
+    w.precalc_sampling()
+    w.init_weights()
+    n_sent, L = ids.shape
+    w.train_ids(ids.reshape(-1), np.arange(0, n_sent * L + 1, L, dtype=np.int64), raw)
+    return scores(words, w.matrix(0), qs, prs, torch.device("cuda", 0))
+
+
+def test_eight_replicas_full_concurrency_quality(tmp_path):
+    """VERDICT r03 "next" 1, scaled down: eight replicas through the class's
+    defaults (gpu_devices = {0 x 8}: auto = model averaging, the automatic
+    cadence — one exchange per Word2Vec::kAutoAverageWords words of a shard —
+    overlapped, every replica a full-concurrency handle, the shared corpus)
+    against one replica at equal tokens, within 1 point both ways. The
+    corpus (400 M tokens, Zipf filler over 200 K ranks, 5 % planted
+    positions, SG-NS d100) is in configs[3]'s regime: a replica's 50 M-token
+    shard alone learns the planted relations (as configs[3]'s 1.25 B-token
+    shards do), which is where periodic model averaging — north_star's
+    multi-GPU design — keeps the single model's scores; DESIGN.md §6.1 has the
+    regime where it does not."""
+    import torch
+
+    from tests.planted_ids import planted_zipf_ids_torch
+
+    data = planted_zipf_ids_torch(400_000_000, 200_000, 0.05, 5, torch.device("cuda", 0))
+    vp = tmp_path / "vocab.txt"
+    vp.write_text("".join(f"{i} {c} {t}\n" for i, (t, c) in enumerate(zip(data[2], data[1]))))
+    one = np.array(_class_on_ids(data, vp, None))
+    eight = np.array(_class_on_ids(data, vp, [0] * 8))
+    d = eight - one
+    print(f"eight replicas (class defaults) vs one: one {one.round(2)} eight {eight.round(2)} delta {d.round(2)}")
+    assert abs(d[0]) <= 1.0 and abs(d[1]) <= 1.0, (one, eight)

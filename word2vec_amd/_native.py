@@ -96,6 +96,7 @@ SIGNATURES = {
     "w2v_dev_row_pitch": (C.c_int, [_P, C.POINTER(_I64)]),
     "w2v_dev_model_layout": (C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), C.POINTER(_I64)]),
     "w2v_dev_upload_corpus": (C.c_int, [_P, _P, _I64, _P, _I64, _I64]),
+    "w2v_dev_share_corpus": (C.c_int, [_P, _P]),
     "w2v_dev_upload_replay": (C.c_int, [_P, _P, _I64, _P, _I64]),
     "w2v_dev_set_progress": (C.c_int, [_P, _I64]),
     "w2v_dev_get_progress": (C.c_int, [_P, C.POINTER(_I64)]),

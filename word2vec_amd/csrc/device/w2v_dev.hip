@@ -129,6 +129,7 @@ struct w2v_dev {
   int64_t n_codes = 0;
   int32_t* ids = nullptr;
   int64_t* soff = nullptr;
+  bool corpus_borrowed = false;    // ids / soff belong to another handle on this device (w2v_dev_share_corpus)
   int64_t n_tok = 0, n_sent = 0, train_words = 0;
   int64_t max_len = 0;        // longest sentence (tokens)
   int64_t* order = nullptr;
@@ -141,6 +142,8 @@ struct w2v_dev {
   float* scratch_f = nullptr;      // x | grad | rows for apply_rows
   uint8_t* scratch_codes = nullptr;
   int64_t scratch_n = 0;           // floats in scratch_f
+  int32_t* wide_scratch = nullptr; // CBOW windows past kMaxWideWindow: per-wave id slices (cbow_center_huge)
+  int64_t wide_scratch_n = 0;      // ints in wide_scratch
   float* xfer_f = nullptr;         // row-sparse transfers: packed rows | row ids
   int64_t xfer_n = 0;
   float fixed_alpha = 0.0f;
@@ -277,7 +280,9 @@ KernelFn kernel_for(const w2v_dev* h) {
     case 6: return w2v::pick_train_nv6(cb, hs, ns, rp, wd);
     case 8: return w2v::pick_train_nv8(cb, hs, ns, rp, wd);
     case 12: return w2v::pick_train_nv12(cb, hs, ns, rp, wd);
-    default: return w2v::pick_train_nv16(cb, hs, ns, rp, wd);
+    case 16: return w2v::pick_train_nv16(cb, hs, ns, rp, wd);
+    case 24: return w2v::pick_train_nv24(cb, hs, ns, rp, wd);
+    default: return w2v::pick_train_nv32(cb, hs, ns, rp, wd);
   }
 }
 
@@ -291,22 +296,38 @@ w2v::ApplyFn apply_for(const w2v_dev* h) {
     case 6: return w2v::pick_apply_nv6();
     case 8: return w2v::pick_apply_nv8();
     case 12: return w2v::pick_apply_nv12();
-    default: return w2v::pick_apply_nv16();
+    case 16: return w2v::pick_apply_nv16();
+    case 24: return w2v::pick_apply_nv24();
+    default: return w2v::pick_apply_nv32();
   }
 }
 
 // Instantiated row widths (floats per lane): the smallest one covering d.
 int pick_nv(int d) {
   const int need = (d + w2v::kWave - 1) / w2v::kWave;
-  static const int widths[] = {1, 2, 3, 4, 5, 6, 8, 12, 16};
+  static const int widths[] = {1, 2, 3, 4, 5, 6, 8, 12, 16, 24, 32};
   for (int w : widths)
     if (w >= need) return w;
-  return 16;
+  return 32;
 }
 
 int set_device(w2v_dev* h) {
   HIP_TRY(hipSetDevice(h->device));
   return W2V_OK;
+}
+
+// Drop the handle's corpus: its own buffers are freed, a borrowed one
+// (w2v_dev_share_corpus) is only released (its owner frees it).
+void release_corpus(w2v_dev* h) {
+  if (!h->corpus_borrowed) {
+    dfree(h->ids);
+    dfree(h->soff);
+  }
+  h->ids = nullptr;
+  h->soff = nullptr;
+  h->corpus_borrowed = false;
+  dfree(h->order);
+  h->corpus_ready = false;
 }
 
 }  // namespace
@@ -318,14 +339,17 @@ const char* w2v_dev_last_error(void) { return g_err.c_str(); }
 
 const char* w2v_dev_knobs(w2v_dev* h) { return h ? h->knobs.desc.c_str() : ""; }
 
-// The per-pair kernels' range: a row is <= 16 floats per lane, a CBOW window
-// span is held <= 4 positions per lane, a context's negatives one per lane.
-constexpr int32_t kMaxDim = 1024, kMaxNegative = 63;
+// The per-pair kernels' range (the reference takes any, Word2Vec.cpp:254, 285,
+// 335): a row is <= 32 floats per lane; a context's negatives are drawn and
+// deduplicated 64 at a time (ns_word_many) with the draw index in the Philox
+// counter (philox_table_pos: k < 2^20); a CBOW window past 127 is walked from
+// the sentence (cbow_center_huge) with a per-wave scratch of huge_stride ints.
+constexpr int32_t kMaxDim = 2048, kMaxNegative = 65535, kMaxWindowHost = 65535;
 
 int w2v_dev_limits(int32_t* max_dim, int32_t* max_window, int32_t* max_negative, int32_t* shared_max_window,
                    int32_t* shared_max_negative) {
   if (max_dim) *max_dim = kMaxDim;
-  if (max_window) *max_window = w2v::kMaxWindow;
+  if (max_window) *max_window = kMaxWindowHost;
   if (max_negative) *max_negative = kMaxNegative;
   if (shared_max_window) *shared_max_window = 8;
   if (shared_max_negative) *shared_max_negative = 15;
@@ -336,11 +360,11 @@ int w2v_dev_create(const w2v_dev_config* cfg, w2v_dev** out) {
   if (!cfg || !out) return fail(W2V_ERR_ARG, "w2v_dev_create: null argument");
   *out = nullptr;
   if (cfg->word_dim <= 0) return fail(W2V_ERR_ARG, "word_dim must be > 0");
-  if (cfg->word_dim > kMaxDim) return fail(W2V_ERR_UNSUPPORTED, "word_dim > 1024 unsupported");
-  if (cfg->window < 0 || cfg->window > w2v::kMaxWindow)
-    return fail(W2V_ERR_UNSUPPORTED, "window must be in [0, 127]");
+  if (cfg->word_dim > kMaxDim) return fail(W2V_ERR_UNSUPPORTED, "word_dim > 2048 unsupported");
+  if (cfg->window < 0 || cfg->window > kMaxWindowHost)
+    return fail(W2V_ERR_UNSUPPORTED, "window must be in [0, 65535]");
   if (cfg->negative < 0 || cfg->negative > kMaxNegative)
-    return fail(W2V_ERR_UNSUPPORTED, "negative must be in [0, 63]");
+    return fail(W2V_ERR_UNSUPPORTED, "negative must be in [0, 65535]");
   if (!cfg->hs && cfg->negative == 0)
     return fail(W2V_ERR_ARG, "neither hs nor negative sampling enabled");
   if (cfg->negative > 0 && cfg->table_size <= 0) return fail(W2V_ERR_ARG, "table_size must be > 0");
@@ -386,9 +410,10 @@ void w2v_dev_destroy(w2v_dev* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (!h->model_bound) { dfree(h->W); dfree(h->C); dfree(h->S); }
   dfree(h->keep); dfree(h->table); dfree(h->codes); dfree(h->points); dfree(h->coff);
-  dfree(h->ids); dfree(h->soff); dfree(h->order); dfree(h->replay); dfree(h->replay_off);
+  if (!h->corpus_borrowed) { dfree(h->ids); dfree(h->soff); }
+  dfree(h->order); dfree(h->replay); dfree(h->replay_off);
   dfree(h->counters); dfree(h->work);
-  dfree(h->scratch_f); dfree(h->scratch_codes); dfree(h->xfer_f);
+  dfree(h->scratch_f); dfree(h->scratch_codes); dfree(h->xfer_f); dfree(h->wide_scratch);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -715,7 +740,7 @@ int w2v_dev_upload_corpus(w2v_dev* h, const int32_t* ids, int64_t n_tok, const i
   }
   if (train_words <= 0 && n_tok > 0) return fail(W2V_ERR_ARG, "train_words must be > 0");
   if (set_device(h)) return W2V_ERR_HIP;
-  dfree(h->ids); dfree(h->soff); dfree(h->order);
+  release_corpus(h);
   HIP_TRY(hipMalloc(&h->ids, (n_tok > 0 ? n_tok : 1) * sizeof(int32_t)));
   if (n_tok > 0) HIP_TRY(hipMemcpy(h->ids, ids, n_tok * sizeof(int32_t), hipMemcpyHostToDevice));
   HIP_TRY(hipMalloc(&h->soff, (n_sent + 1) * sizeof(int64_t)));
@@ -753,7 +778,7 @@ int w2v_dev_adopt_corpus(w2v_dev* h, w2v_ingest* g) {
   }
   std::vector<int64_t> hist((size_t)h->V, 0);
   for (int64_t w = 0; w < v.n_vocab; ++w) hist[(size_t)w] = v.hist[w];
-  dfree(h->ids); dfree(h->soff); dfree(h->order);
+  release_corpus(h);
   HIP_TRY(hipMalloc(&h->ids, (v.n_ids > 0 ? v.n_ids : 1) * sizeof(int32_t)));
   if (v.n_ids > 0) HIP_TRY(hipMemcpy(h->ids, v.ids, v.n_ids * sizeof(int32_t), hipMemcpyDeviceToDevice));
   HIP_TRY(hipMalloc(&h->soff, (v.n_sentences + 1) * sizeof(int64_t)));
@@ -765,6 +790,30 @@ int w2v_dev_adopt_corpus(w2v_dev* h, w2v_ingest* g) {
   h->max_len = max_len;
   h->train_words = v.train_words;
   h->tok_count.swap(hist);
+  ++h->data_version;
+  h->corpus_ready = true;
+  return W2V_OK;
+}
+
+int w2v_dev_share_corpus(w2v_dev* h, w2v_dev* src) {
+  w2v::Range range_("w2v_dev_share_corpus");
+  if (!h || !src || h == src) return fail(W2V_ERR_ARG, "w2v_dev_share_corpus: two distinct handles");
+  if (!src->corpus_ready) return fail(W2V_ERR_STATE, "w2v_dev_share_corpus: the source has no corpus");
+  if (src->device != h->device) return fail(W2V_ERR_ARG, "w2v_dev_share_corpus: the source is on another device");
+  if (h->V != src->V) return fail(W2V_ERR_ARG, "w2v_dev_share_corpus: the vocabularies differ");
+  if (set_device(h)) return W2V_ERR_HIP;
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  release_corpus(h);
+  HIP_TRY(hipMalloc(&h->order, (src->n_sent > 0 ? src->n_sent : 1) * sizeof(int64_t)));
+  h->ids = src->ids;
+  h->soff = src->soff;
+  h->corpus_borrowed = true;
+  h->n_tok = src->n_tok;
+  h->n_sent = src->n_sent;
+  h->n_order = 0;
+  h->max_len = src->max_len;
+  h->train_words = src->train_words;
+  h->tok_count = src->tok_count;
   ++h->data_version;
   h->corpus_ready = true;
   return W2V_OK;
@@ -1340,6 +1389,21 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   h->last_flush = a.priv_n > 0 ? a.flush_every : 0;
   h->last_ctx_flush = a.ctx_n > 0 ? a.ctx_flush_every : 0;
   priv_scales(h, a, h->knobs.scale_resident ? resident_wg : (int64_t)grid.x, false);
+  a.wide_ids = nullptr;
+  a.wide_stride = 0;
+  if (h->cfg.cbow && h->cfg.window > w2v::kMaxWideWindow) {  // cbow_center_huge: one id slice per wave
+    const int64_t stride = w2v::huge_stride(h->cfg.window);
+    const int64_t need = (int64_t)grid.x * (int64_t)(block.x / w2v::kWave) * stride;
+    if (need > h->wide_scratch_n) {
+      HIP_TRY(hipStreamSynchronize(h->stream));  // an earlier launch may still use the old slices
+      dfree(h->wide_scratch);
+      h->wide_scratch_n = 0;
+      HIP_TRY(hipMalloc(&h->wide_scratch, (size_t)need * sizeof(int32_t)));
+      h->wide_scratch_n = need;
+    }
+    a.wide_ids = h->wide_scratch;
+    a.wide_stride = stride;
+  }
   hipLaunchKernelGGL(fn, grid, block, lds_bytes, h->stream, a);
   HIP_TRY(hipGetLastError());
   return W2V_OK;

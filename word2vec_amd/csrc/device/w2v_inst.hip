@@ -12,7 +12,7 @@
 
 namespace w2v {
 
-constexpr int kMaxT = 8;
+constexpr int kMaxT = W2V_NV <= 16 ? 8 : 4;  // d > 1024: 4 target rows per batch
 
 // wide: CBOW with 2 * window + 1 > 64 (skip-gram takes any window in one kernel)
 KernelFn W2V_CAT(pick_train_nv, W2V_NV)(bool cbow, bool hs, bool ns, bool replay, bool wide) {

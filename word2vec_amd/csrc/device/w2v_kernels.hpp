@@ -63,7 +63,7 @@ constexpr int kMaxBlock = NV <= 6 ? 1024 : 256;
 // CU when a row is <= 2 floats per lane (d <= 128: 64 VGPRs), else one.
 #ifndef W2V_MIN_WAVES
 template <int NV>
-constexpr int kMinWaves = NV <= 2 ? 8 : 4;
+constexpr int kMinWaves = NV <= 2 ? 8 : NV <= 16 ? 4 : 2;  // d > 1024: 256 VGPRs
 #else  // occupancy experiments (tools/r02/occ_probe.sh)
 template <int NV>
 constexpr int kMinWaves = W2V_MIN_WAVES;
@@ -111,6 +111,8 @@ struct TrainArgs {
   const float* ctx_M;          // CBOW: context matrix whose rows [0, ctx_n) are privatised too (or null)
   int32_t ctx_n;
   int32_t ctx_flush_every;     // centers of the workgroup between flushes of the context rows
+  int32_t* wide_ids;           // CBOW, window > kMaxWideWindow: per wave a slice of wide_stride ints (cbow_center_huge)
+  int64_t wide_stride;
   int64_t item0;               // shared-negatives kernel: work items are order[item0 + k] (or item0 + k)
   int64_t hot_atomic;          // shared-negatives kernel: W / C rows [0, hot_atomic) take memory-side atomic deltas
   int32_t nseg;                // work items per sentence (parallel Philox schedule; 1 = whole sentences)
@@ -207,10 +209,13 @@ __device__ __forceinline__ float canonical_f(uint32_t x) {
   return r >= 1.0f ? __int_as_float(0x3F7FFFFF) : r;
 }
 
+// Draw k of context slot `slot`: counter (position, sentence, slot << 8 | k's
+// low byte, epoch ^ (k's high bits << 20)); for k < 256 (every negative up to
+// 255) the last word is the epoch alone.
 __device__ __forceinline__ uint32_t philox_table_pos(const TrainArgs& a, uint32_t s, uint32_t i,
                                                      uint32_t slot, uint32_t k) {
   uint32_t o0, o1, o2, o3;
-  philox(i, s, (slot << 8) | k, a.epoch, a.key0, a.key1, o0, o1, o2, o3);
+  philox(i, s, (slot << 8) | (k & 255u), a.epoch ^ ((k >> 8) << 20), a.key0, a.key1, o0, o1, o2, o3);
   const uint64_t x = ((uint64_t)o1 << 32) | o0;
   return (uint32_t)__umul64hi(x, (uint64_t)a.table_size);
 }
@@ -759,6 +764,63 @@ __device__ __forceinline__ void ns_word(const TrainArgs& a, float* M, int word, 
   apply_list<NV, MAXT>(a, M, T, tgt_l, (lane == 0) ? 0 : 1, x, g, alpha, cnt, pr);
 }
 
+// ---------------------------------------------------------------------------
+// NS with more draws than a wave has lanes (negative >= 64; the reference
+// takes any value, Word2Vec.cpp:254-255). The targets keep the set semantics
+// and the order of ns_targets — the positive, then the first occurrence of
+// every negative that differs from it, in draw order — taken 64 draws at a
+// time: chunk ch holds draws k = 64 ch + lane; a draw is a duplicate if an
+// earlier draw of its chunk or any draw of an earlier chunk (drawn again: the
+// same counter gives the same word) is the same word. Each chunk's new
+// targets are applied before the next chunk's are found (a duplicate test
+// needs only the words, not the rows).
+// ---------------------------------------------------------------------------
+template <bool REPLAY>
+__device__ __forceinline__ int draw_chunk(const TrainArgs& a, uint32_t s, uint32_t i, int slot, int ch, int lane,
+                                          const uint32_t* rp) {
+  const int k = kWave * ch + lane;
+  int w = -1;
+  if (k < a.negative) {
+    const uint32_t pos = REPLAY ? rp[k] : philox_table_pos(a, s, i, (uint32_t)slot, (uint32_t)k);
+    w = (int)a.table[pos];
+  }
+  return w;
+}
+
+template <int NV, int MAXT, bool REPLAY>
+__device__ __forceinline__ void ns_word_many(const TrainArgs& a, float* M, int word, uint32_t s, uint32_t i, int slot,
+                                          int lane, const float (&x)[NV], float (&g)[NV], float alpha,
+                                          Counters& cnt, float* lds, const uint32_t*& rp) {
+  const PrivRows pr = (a.priv_M == M) ? out_rows<NV>(a, lds) : PrivRows();
+  const int neg = a.negative;
+  const int nch = (neg + kWave - 1) / kWave;
+  apply_list<NV, MAXT>(a, M, 1, word, 0, x, g, alpha, cnt, pr);  // the positive (label 1)
+  for (int ch = 0; ch < nch; ++ch) {
+    const int w = draw_chunk<REPLAY>(a, s, i, slot, ch, lane, rp);
+    bool dup = (w < 0) || (w == word);
+    for (int j = 0; j < kWave - 1; ++j) {
+      const int v = readlane_i(w, j);
+      dup = dup || (lane > j && v == w);
+    }
+    for (int c2 = 0; c2 < ch; ++c2) {
+      const int wp = draw_chunk<REPLAY>(a, s, i, slot, c2, lane, rp);
+      for (int j = 0; j < kWave; ++j) dup = dup || (readlane_i(wp, j) == w);
+    }
+    unsigned long long uniq = ballot(!dup);
+    int tgt_l = 0, m = 0;
+    while (uniq) {
+      const int b = __builtin_ctzll(uniq);
+      uniq &= uniq - 1;
+      const int v = readlane_i(w, b);
+      if (lane == m) tgt_l = v;
+      ++m;
+    }
+    if (m > 0) apply_list<NV, MAXT>(a, M, m, tgt_l, 1, x, g, alpha, cnt, pr);  // negatives (label 0)
+  }
+  cnt.draws += (unsigned long long)neg;
+  if (REPLAY) rp += neg;
+}
+
 // Draw table words for `ndraw` (slot, k) pairs starting at slot `slot0`:
 // lane t -> slot0 + t / neg, k = t % neg.
 template <bool REPLAY>
@@ -836,7 +898,9 @@ __device__ __forceinline__ void sg_center(const TrainArgs& a, float* lds, const 
     if (j == i) continue;
     const int w = (j - lo < kWave) ? readlane_i(ctx_l, j - lo) : uniform_i(sent[j]);  // window > 31: span > 64
     if (HS) hs_word<NV, MAXT>(a, w, lane, x, g, alpha, cnt, lds);
-    if (NS) {
+    if (NS && neg >= kWave) {
+      ns_word_many<NV, MAXT, REPLAY>(a, a.C, w, s, (uint32_t)i, slot, lane, x, g, alpha, cnt, lds, rp);
+    } else if (NS) {
       const int gs = slot % G;
       if (gs == 0) {
         const int nd = min(G, nctx - slot) * neg;
@@ -890,7 +954,9 @@ __device__ __forceinline__ void cbow_tail(const TrainArgs& a, float* lds, int i,
   }
   cnt.stamp(2);
   if (HS) hs_word<NV, MAXT>(a, c, lane, h, g, alpha, cnt, lds);
-  if (NS) {
+  if (NS && a.negative >= kWave) {
+    ns_word_many<NV, MAXT, REPLAY>(a, a.W, c, s, (uint32_t)i, 0, lane, h, g, alpha, cnt, lds, rp);
+  } else if (NS) {
     const int nd = a.negative;
     const int negw_l = draw_negatives<REPLAY>(a, s, (uint32_t)i, 0, nd, lane, rp);
     cnt.draws += (unsigned long long)nd;
@@ -1047,15 +1113,95 @@ __device__ __forceinline__ void cbow_center_wide(const TrainArgs& a, float* lds,
                                       rp, cnt, lane);
 }
 
-constexpr int kWideChunks = 4;  // wide-window CBOW kernels: window <= 32 * kWideChunks - 1
-constexpr int kMaxWindow = 32 * kWideChunks - 1;
+constexpr int kWideChunks = 4;  // wide-window CBOW kernels: window <= 32 * kWideChunks - 1 in registers
+constexpr int kMaxWideWindow = 32 * kWideChunks - 1;
+// Any larger window (the reference takes any, Word2Vec.cpp:285): cbow_center_huge.
+constexpr int kMaxWindow = (1 << 20) - 1;
+// Ints of a wave's cbow_center_huge scratch slice for `window`: the unique
+// ids (<= 2 window) and one 64-bit unique mask per 64 span positions.
+__host__ __device__ inline int64_t huge_stride(int window) {
+  const int64_t span = 2 * (int64_t)window + 1;
+  return 2 * (int64_t)window + 2 * ((span + 63) / 64) + 2;
+}
+
+// CBOW center for windows past kMaxWideWindow: the same set semantics and
+// ascending visiting order as cbow_center, with the span read from the
+// sentence 64 positions at a time. Pass 1 marks each position that is not a
+// repeat of an earlier valid one (a scalar walk over the earlier positions)
+// and keeps each chunk's unique mask in this wave's slice of a global scratch;
+// pass 2 ranks every unique id among all of them (the count of smaller ones)
+// and writes it to slot `rank`, so the slice holds the ids in ascending order
+// for cbow_tail. O(span^2 / 64) scalar steps per center: the price of a window
+// no register set holds.
+template <int NV, int MAXT, bool HS, bool NS, bool REPLAY>
+__device__ __forceinline__ void cbow_center_huge(const TrainArgs& a, float* lds, const int32_t* sent, int len, int i,
+                                                 int c, int rw, uint32_t s, float alpha, const uint32_t*& rp,
+                                                 Counters& cnt, int lane) {
+  const int lo = max(0, i - a.window + rw), hi = min(len, i + a.window + 1 - rw);
+  const int n = hi - lo - 1;
+  if (n <= 0) return;
+  const int span = hi - lo;
+  const int me = i - lo;
+  const int nch = (span + kWave - 1) / kWave;
+  const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  int32_t* ids_out = a.wide_ids + wave * a.wide_stride;
+  int32_t* masks = ids_out + 2 * (int64_t)a.window;  // 2 ints per chunk
+  int U = 0;
+  for (int ch = 0; ch < nch; ++ch) {
+    const int p = kWave * ch + lane;
+    const bool valid = p < span && p != me;
+    const int id = valid ? sent[lo + p] : -1;
+    bool dup = !valid;
+    const int jmax = min(span, kWave * ch + kWave - 1);
+    for (int j = 0; j < jmax; ++j) {
+      if (j == me) continue;
+      const int v = uniform_i(sent[lo + j]);
+      dup = dup || (j < p && v == id);
+    }
+    const unsigned long long uq = ballot(!dup);
+    U += __popcll(uq);
+    if (lane == 0) {
+      masks[2 * ch] = (int32_t)(uint32_t)uq;
+      masks[2 * ch + 1] = (int32_t)(uint32_t)(uq >> 32);
+    }
+  }
+  drain_vmem();
+  for (int ch = 0; ch < nch; ++ch) {
+    const int p = kWave * ch + lane;
+    const int id = (p < span) ? sent[lo + p] : -1;
+    const unsigned long long mine =
+        ((unsigned long long)(uint32_t)__hip_atomic_load(masks + 2 * ch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 32) |
+        (uint32_t)__hip_atomic_load(masks + 2 * ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool uniq = (mine >> lane) & 1ull;
+    int rank = 0;
+    for (int c2 = 0; c2 < nch; ++c2) {
+      unsigned long long m =
+          ((unsigned long long)(uint32_t)__hip_atomic_load(masks + 2 * c2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 32) |
+          (uint32_t)__hip_atomic_load(masks + 2 * c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      m = ((unsigned long long)(uint32_t)readlane_i((int)(m >> 32), 0) << 32) | (uint32_t)readlane_i((int)(uint32_t)m, 0);
+      while (m) {
+        const int b = __builtin_ctzll(m);
+        m &= m - 1;
+        rank += (uniform_i(sent[lo + kWave * c2 + b]) < id) ? 1 : 0;
+      }
+    }
+    if (uniq) ids_out[rank] = id;
+  }
+  drain_vmem();
+  cbow_tail<NV, MAXT, HS, NS, REPLAY>(
+      a, lds, i, c, n, U,
+      [&](int r) { return uniform_i(__hip_atomic_load(ids_out + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)); },
+      s, alpha, rp, cnt, lane);
+}
 
 template <int NV, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY, bool WIDE>
 __device__ __forceinline__ void center(const TrainArgs& a, float* lds, const int32_t* sent, int len, int i, int c,
                                        int rw, uint32_t s, float alpha, const uint32_t*& rp, Counters& cnt,
                                        int lane) {
   cnt.stamp(0);
-  if (CBOW && WIDE)
+  if (CBOW && WIDE && a.window > kMaxWideWindow)
+    cbow_center_huge<NV, MAXT, HS, NS, REPLAY>(a, lds, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
+  else if (CBOW && WIDE)
     cbow_center_wide<NV, MAXT, HS, NS, REPLAY, kWideChunks>(a, lds, sent, len, i, c, rw, s, alpha, rp, cnt, lane);
   else if (CBOW)
     cbow_center<NV, MAXT, HS, NS, REPLAY>(a, lds, sent, len, i, c, rw, s, alpha, rp, cnt, lane);

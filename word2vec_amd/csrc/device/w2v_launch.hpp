@@ -20,6 +20,8 @@ W2V_DECLARE_NV(6)
 W2V_DECLARE_NV(8)
 W2V_DECLARE_NV(12)
 W2V_DECLARE_NV(16)
+W2V_DECLARE_NV(24)
+W2V_DECLARE_NV(32)
 #undef W2V_DECLARE_NV
 
 // Shared-negatives minibatch SG (w2v_shared.hip) for a row pitch (floats, a

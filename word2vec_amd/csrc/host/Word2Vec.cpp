@@ -524,9 +524,9 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
   auto release = [&]() {
     if (grp) w2v_group_destroy(grp);
     grp = nullptr;
-    for (auto*& r : reps) {
-      if (r) w2v_dev_destroy(r);
-      r = nullptr;
+    for (size_t i = reps.size(); i-- > 0;) {  // borrowers of a shared corpus before its owner
+      if (reps[i]) w2v_dev_destroy(reps[i]);
+      reps[i] = nullptr;
     }
   };
   try {
@@ -543,9 +543,15 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
       check(w2v_dev_upload_model(reps[i], W.data(), uses_C() ? C.data() : nullptr,
                                  train_method == "hs" ? synapses1.data() : nullptr),
             "w2v_dev_upload_model");
-      check(w2v_dev_upload_corpus(reps[i], ids.data(), (int64_t)ids.size(), offsets.data(), n,
-                                  std::max<int64_t>(1, train_words)),
-            "w2v_dev_upload_corpus");
+      size_t owner = i;  // replicas sharing a device share one resident corpus (w2v_dev_share_corpus)
+      for (size_t j = 0; j < i && owner == i; ++j)
+        if (gpu_devices[j] == gpu_devices[i]) owner = j;
+      if (owner != i)
+        check(w2v_dev_share_corpus(reps[i], reps[owner]), "w2v_dev_share_corpus");
+      else
+        check(w2v_dev_upload_corpus(reps[i], ids.data(), (int64_t)ids.size(), offsets.data(), n,
+                                    std::max<int64_t>(1, train_words)),
+              "w2v_dev_upload_corpus");
       check(w2v_dev_set_train_words(reps[i], std::max<int64_t>(1, train_words / (int64_t)R)),
             "w2v_dev_set_train_words");
       apply_policy(reps[i]);
@@ -578,8 +584,15 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
         largest = std::max(largest, cum[i].back());
         check(w2v_dev_set_order(reps[i], shard[i].data(), (int64_t)shard[i].size()), "w2v_dev_set_order");
       }
+      // auto cadence: summing (two replicas) converges to the one model as
+      // rounds shorten, so kAutoReplicaRounds per epoch; averaging (more
+      // replicas) wants LONG rounds — a round's mean divides the progress of
+      // every row only one replica touched in it by R — so at most one
+      // exchange per kAutoAverageWords words of a shard
+      const int64_t avg_rounds = std::max<int64_t>(1, largest / kAutoAverageWords);
       const int64_t rounds = sync_words > 0 ? std::max<int64_t>(1, (largest + sync_words - 1) / sync_words)
-                                            : std::max<int64_t>(1, std::min<int64_t>(auto_rounds, largest));
+                             : mode == W2V_GROUP_SUM ? std::max<int64_t>(1, std::min<int64_t>(auto_rounds, largest))
+                                                     : std::min<int64_t>(auto_rounds, avg_rounds);
       for (int64_t r = 0; r < rounds; ++r) {
         int64_t words = 0;
         for (size_t i = 0; i < R; ++i) {

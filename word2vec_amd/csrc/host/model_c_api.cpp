@@ -276,4 +276,16 @@ int w2v_model_read_vocab(w2v_model* m, const char* path) {
   return guard(m, [&] { m->w.read_vocab(path); });
 }
 
+// The reference's public vocabulary products (Word2Vec.h:70-72), e.g. after
+// read_vocab, which builds none of them (Word2Vec.cpp:171-196).
+int w2v_model_create_huffman_tree(w2v_model* m) {
+  return guard(m, [&] { m->w.create_huffman_tree(); });
+}
+int w2v_model_make_table(w2v_model* m) {
+  return guard(m, [&] { m->w.make_table(); });
+}
+int w2v_model_precalc_sampling(w2v_model* m) {
+  return guard(m, [&] { m->w.precalc_sampling(); });
+}
+
 }  // extern "C"

@@ -137,6 +137,11 @@ class DeviceTrainer:
                   "w2v_dev_upload_corpus")
         self.n_sent = o.size - 1
 
+    def share_corpus(self, src: "DeviceTrainer"):
+        """Train on src's resident corpus (same device and vocab; no copy; src must outlive this handle)."""
+        self._chk(self.lib.w2v_dev_share_corpus(self.h, src.h), "w2v_dev_share_corpus")
+        self.n_sent = src.n_sent
+
     def adopt_corpus(self, ingest):
         """w2v_dev_adopt_corpus: the samples of a mapped GpuIngest (word2vec_amd/ingest.py), device to device."""
         self._chk(self.lib.w2v_dev_adopt_corpus(self.h, ingest.g), "w2v_dev_adopt_corpus")

@@ -62,6 +62,9 @@ def _load():
             "w2v_model_save": (C.c_int, [P, S, I32, I32]),
             "w2v_model_load": (C.c_int, [P, S, I32]),
             "w2v_model_save_vocab": (C.c_int, [P, S]),
+            "w2v_model_create_huffman_tree": (C.c_int, [P]),
+            "w2v_model_make_table": (C.c_int, [P]),
+            "w2v_model_precalc_sampling": (C.c_int, [P]),
             "w2v_model_save_checkpoint": (C.c_int, [P, S]),
             "w2v_model_load_checkpoint": (C.c_int, [P, S]),
             "w2v_model_set_checkpoint_path": (C.c_int, [P, S]),
@@ -226,6 +229,15 @@ class Word2Vec:
 
     def read_vocab(self, path):
         self._chk(self.L.w2v_model_read_vocab(self.h, str(path).encode()), "read_vocab")
+
+    def create_huffman_tree(self):
+        self._chk(self.L.w2v_model_create_huffman_tree(self.h), "create_huffman_tree")
+
+    def make_table(self):
+        self._chk(self.L.w2v_model_make_table(self.h), "make_table")
+
+    def precalc_sampling(self):
+        self._chk(self.L.w2v_model_precalc_sampling(self.h), "precalc_sampling")
 
     # introspection ---------------------------------------------------------
     @property
