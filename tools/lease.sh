@@ -11,7 +11,8 @@
 #   profile:<cN>              tools/profile.sh (kernel trace + FETCH_SIZE + WRITE_SIZE passes) +
 #                             tools/pmc_summary.py -> profiles/<tag>_<cN>_* and profiles/pmc_traffic.json
 #   pmc:<cN>[:<passes>]       tools/pmc.sh counter passes (default sq1 sq2 tcc atom)
-#   py:<script>[:<args>]      python3 -u <script> <args> (600 s)
+#   py:<script>[:<args>]      python3 -u <script> <args> (600 s; LEASE_PY_TIMEOUT overrides)
+#   sh:<script>[:<args>]      bash <script> <args> (900 s), e.g. sh:tools/r03/ab.sh:<tag> <variant> "c3 c1" 2
 # Outputs: gpurun_out/<tag>_*; profiles written on the box come back under
 # gpurun_out/<tag>_profiles/ (copy them into profiles/ to commit).
 set -o pipefail
@@ -45,8 +46,11 @@ for step in "$@"; do
       python tools/pmc_table.py ${TAG}_$a > $OUT/${TAG}_pmc_table_$a.log 2>&1 || true
       cat $OUT/${TAG}_pmc_table_$a.log ;;
     py)
-      timeout -k 10 600 python3 -u $a $b > $OUT/${TAG}_$(basename $a .py).log 2>&1 || stop "$step" $?
-      tail -5 $OUT/${TAG}_$(basename $a .py).log ;;
+      timeout -k 10 ${LEASE_PY_TIMEOUT:-600} python3 -u $a $b > $OUT/${TAG}_$(basename $a .py).log 2>&1 || stop "$step" $?
+      tail -12 $OUT/${TAG}_$(basename $a .py).log ;;
+    sh)
+      eval "timeout -k 10 900 bash $a $b" > $OUT/${TAG}_$(basename $a .sh).log 2>&1 || stop "$step" $?
+      tail -20 $OUT/${TAG}_$(basename $a .sh).log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

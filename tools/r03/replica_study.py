@@ -32,92 +32,11 @@ from word2vec_amd import _native as N  # noqa: E402
 from word2vec_amd import host  # noqa: E402
 from word2vec_amd.device import Config, DeviceTrainer  # noqa: E402
 from word2vec_amd.replicas import NativeAverager  # noqa: E402
-
-
-def planted_zipf_ids(n_tokens, sent_len=1000, filler=100_000, rows=50, cols=4, topic=8, role=8, planted_frac=0.10,
-                     seed=0):
-    """tests/quality.py planted_zipf_corpus as raw ids (vectorised): filler ids
-    [0, filler), entities, topics, roles after it."""
-    rng = np.random.default_rng(seed)
-    n_sent = n_tokens // sent_len
-    E0 = filler
-    T0 = E0 + rows * cols
-    R0 = T0 + rows * topic
-    n_raw = R0 + cols * role
-    p = 1.0 / np.arange(1, filler + 1)
-    cdf = np.cumsum(p)
-    cdf /= cdf[-1]
-    tok = np.searchsorted(cdf, rng.random(n_sent * sent_len), side="right").clip(0, filler - 1).astype(np.int64)
-    si = rng.integers(rows, size=n_sent)
-    sj = rng.integers(cols, size=n_sent)
-    pos = np.flatnonzero(rng.random(n_sent * sent_len) < planted_frac)
-    s = pos // sent_len
-    i, j = si[s], sj[s]
-    kind = rng.random(pos.size)
-    ent = kind < 0.34
-    top = (kind >= 0.34) & (kind < 0.67)
-    rol = kind >= 0.67
-    # entity: the sentence's (i, j) w.p. 0.75, else a same-row or same-column neighbour
-    r1 = rng.random(pos.size)
-    r2 = rng.random(pos.size)
-    ei, ej = i.copy(), j.copy()
-    cross = r1 <= 0.25
-    rowx = cross & (r2 < 0.5)
-    colx = cross & (r2 >= 0.5)
-    ej[rowx] = rng.integers(cols, size=int(rowx.sum()))
-    ei[colx] = rng.integers(rows, size=int(colx.sum()))
-    out = np.empty(pos.size, np.int64)
-    out[ent] = E0 + ei[ent] * cols + ej[ent]
-    out[top] = T0 + i[top] * topic + rng.integers(topic, size=int(top.sum()))
-    out[rol] = R0 + j[rol] * role + rng.integers(role, size=int(rol.sum()))
-    tok[pos] = out
-    names = ([f"f{k}" for k in range(filler)] + [f"e{a}_{b}" for a in range(rows) for b in range(cols)]
-             + [f"t{a}_{k}" for a in range(rows) for k in range(topic)]
-             + [f"r{b}_{k}" for b in range(cols) for k in range(role)])
-    assert len(names) == n_raw
-    qs = [(f"e{a}_{l}", f"e{a}_{b}", f"e{c}_{l}", f"e{c}_{b}") for a in range(rows) for c in range(rows) if a != c
-          for b in range(cols) for l in range(cols) if b != l]
-    prs = []
-    for a in range(rows):
-        for b in range(cols):
-            for c in range(rows):
-                for d in range(cols):
-                    if (a, b) < (c, d) and rng.random() < 0.05:
-                        prs.append((f"e{a}_{b}", f"e{c}_{d}", float((a == c) + (b == d))))
-    return tok, n_sent, names, qs, prs
-
-
-def build(tok, n_sent, sent_len, names, min_count=5):
-    counts = np.bincount(tok, minlength=len(names))
-    order = np.argsort(-counts, kind="stable")
-    V = int((counts >= min_count).sum())
-    vr = order[:V]
-    remap = np.full(len(names), -1, np.int64)
-    remap[vr] = np.arange(V)
-    ids = remap[tok]
-    keep = ids >= 0
-    lens = keep.reshape(n_sent, sent_len).sum(1)
-    soff = np.zeros(n_sent + 1, np.int64)
-    soff[1:] = np.cumsum(lens)
-    return ids[keep].astype(np.int32), soff, counts[vr].astype(np.int64), [names[k] for k in vr]
+from tests.planted_ids import build, planted_zipf_ids, scores  # noqa: E402
 
 
 def gpu_scores(words, E, qs, prs, dev):
-    idx = {w: k for k, w in enumerate(words)}
-    En = torch.tensor(E, device=dev)
-    En = En / En.norm(dim=1, keepdim=True).clamp_min(1e-12)
-    Q = torch.tensor([[idx[x] for x in q] for q in qs if all(x in idx for x in q)], device=dev)
-    correct = 0
-    for s in range(0, Q.shape[0], 4096):
-        qa, qb, qc, qd = Q[s:s + 4096].T
-        sims = (En[qb] - En[qa] + En[qc]) @ En.T
-        r = torch.arange(qa.numel(), device=dev)
-        for ex in (qa, qb, qc):
-            sims[r, ex] = -float("inf")
-        correct += int((sims.argmax(1) == qd).sum())
-    from word2vec_amd.evaluate import similarity_score
-
-    return 100.0 * correct / max(1, Q.shape[0]), similarity_score(words, E, prs)["spearman"]
+    return scores(words, E, qs, prs, dev)
 
 
 def train(args, R, rounds, gmode, overlap, seed, data, dev):
