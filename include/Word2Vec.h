@@ -28,6 +28,42 @@ using w2v_dense::IOFormat;
 using w2v_dense::RMatrixXf;
 using w2v_dense::RowVectorXf;
 
+// Drop-in compatibility with the reference header's environment
+// (/root/reference/Word2Vec.h:4-24): its callers — the reference's own
+// main.cpp — compile against the standard headers it includes, `using
+// namespace std` / `using namespace Eigen`, Eigen::initParallel()
+// (main.cpp:96) and omp_set_num_threads (main.cpp:186, declared by the
+// <omp.h> Eigen pulls in under the reference's -fopenmp). Here: the same
+// standard headers, both using-directives over a minimal namespace Eigen
+// (initParallel is a no-op: nothing here runs Eigen's threads), and <omp.h>
+// under -fopenmp. The reference's main.cpp then compiles unmodified against
+// include/ (tests/test_class_host.py::test_reference_caller_compiles).
+// Define W2V_NO_REFERENCE_ENVIRONMENT to keep all of this out (a translation
+// unit that includes the real Eigen must include it first or define it).
+#ifndef W2V_NO_REFERENCE_ENVIRONMENT
+#include <algorithm>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <iterator>
+#include <list>
+#include <numeric>
+#include <set>
+#include <sstream>
+#include <tuple>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+#ifndef EIGEN_WORLD_VERSION  // the real Eigen is not in this translation unit
+namespace Eigen {
+inline void initParallel() {}
+using w2v_dense::IOFormat;
+}  // namespace Eigen
+#endif
+using namespace std;
+using namespace Eigen;
+#endif
+
 class Word2Vec {
  public:
   int iter;

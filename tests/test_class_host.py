@@ -313,3 +313,39 @@ def test_hyperparameter_limits_fail_early():
     assert r.returncode == 1 and "Please set -size in [1, 2048]" in r.stdout
     r = _cli("-negative", "16", "-shared-negatives", "1")
     assert r.returncode == 1 and "-shared-negatives 1" in r.stdout
+
+
+def _compile_caller(src_args, out, cwd):
+    """g++ with the reference's own build line (main.cpp:2, minus -march and
+    the Eigen path) against include/ and the product libraries."""
+    lib = ROOT / "word2vec_amd" / "lib"
+    cmd = ["g++", "-std=c++11", "-O2", "-fopenmp", *src_args, "-I", str(ROOT / "include"), "-o", str(out),
+           "-L", str(lib), "-lword2vec_amd", "-lw2v_hip", f"-Wl,-rpath,{lib}"]
+    return subprocess.run(cmd, capture_output=True, text=True, cwd=cwd, timeout=300)
+
+
+def test_reference_shaped_caller_compiles(tmp_path):
+    """a caller written against the reference's API and
+    environment (tests/callers/ref_caller.cpp: Eigen::initParallel,
+    omp_set_num_threads, unqualified std names) compiles and links against
+    include/Word2Vec.h and the product libraries unmodified (it runs on the
+    GPU in tests/test_gpu_class.py)."""
+    r = _compile_caller([str(ROOT / "tests" / "callers" / "ref_caller.cpp")], tmp_path / "ref_caller", tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
+def test_reference_caller_compiles(tmp_path):
+    """The reference's own main.cpp (read from /root/reference as text, fed to
+    the compiler on stdin so its directory's Word2Vec.h is not found) compiles
+    and links against include/ unmodified: the drop-in header provides the
+    environment it relies on. Container only: the GPU box has
+    no /root/reference."""
+    src = Path("/root/reference/main.cpp")
+    if not src.exists():
+        pytest.skip("reference not present (GPU box)")
+    lib = ROOT / "word2vec_amd" / "lib"
+    cmd = ["g++", "-std=c++11", "-O2", "-fopenmp", "-x", "c++", "-", "-I", str(ROOT / "include"), "-o",
+           str(tmp_path / "ref_main"), "-L", str(lib), "-lword2vec_amd", "-lw2v_hip", f"-Wl,-rpath,{lib}"]
+    r = subprocess.run(cmd, input=src.read_text(encoding="utf-8-sig"), capture_output=True, text=True,
+                       cwd=tmp_path, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]

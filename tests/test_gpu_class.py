@@ -204,3 +204,36 @@ def test_checkpoint_resume_continues(tmp_path):
     step_first = np.abs(W1 - W0).mean()
     assert np.isfinite(c.matrix(0)).all()
     assert step_new > 0.25 * step_first, (step_new, step_first)
+
+
+@pytest.mark.parametrize("model,method", [("sg", "ns"), ("cbow", "hs")])
+def test_reference_shaped_caller_trains(tmp_path, model, method):
+    """tests/callers/ref_caller.cpp — the reference CLI's
+    call sequence and environment, written against the reference API only —
+    built here against include/Word2Vec.h and run on the GPU: it writes the
+    reference's vocab file (index count text) and vector file ("rows cols"
+    header, one word and its d values per line, W or C by mode as
+    main.cpp:196-201) for the corpus's vocabulary, with finite trained values."""
+    from tests.test_class_host import _compile_caller
+
+    exe = tmp_path / "ref_caller"
+    r = _compile_caller([str(Path(__file__).parent / "callers" / "ref_caller.cpp")], exe, tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    sents = zipf_sentences(40, 150, 400, seed=61, ragged=True)
+    corpus = tmp_path / "corpus.txt"
+    corpus.write_text("\n".join(" ".join(s) for s in sents) + "\n")
+    r = subprocess.run([str(exe), str(corpus), str(tmp_path / "vec.txt"), str(tmp_path / "vocab.txt"), model, method],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    w = Word2Vec(iter=1, window=5, min_count=2, table_size=100000, word_dim=32, negative=5 if method == "ns" else 0,
+                 subsample_threshold=1e-3, init_alpha=0.05, min_alpha=2.5e-6, cbow_mean=True, train_method=method,
+                 model=model)
+    w.build_vocab(sents)
+    words, counts = w.vocab()
+    assert (tmp_path / "vocab.txt").read_text().splitlines() == [f"{i} {c} {t}" for i, (t, c) in
+                                                                 enumerate(zip(words, counts))]
+    lines = (tmp_path / "vec.txt").read_text().splitlines()
+    assert lines[0] == f"{len(words)} 32"
+    assert [ln.split()[0] for ln in lines[1:]] == words
+    vals = np.array([[float(x) for x in ln.split()[1:]] for ln in lines[1:]])
+    assert vals.shape == (len(words), 32) and np.isfinite(vals).all() and np.abs(vals).max() > 0

@@ -383,6 +383,15 @@ __device__ __forceinline__ void priv_add(const PrivRows& pr, int64_t row, int d,
   if (lane == 0) atomicOr(pr.dirty + (p >> 6), 1ull << (p & 63));
 }
 
+// NS's sigma, Word2Vec.cpp:263: f = 1.0 / (1 + exp(-f)) — a float sum 1 + e
+// divided in double and rounded back to the float f. For a float x, the
+// double quotient 1.0 / x rounded to float IS the correctly rounded float
+// quotient 1.0f / x (double rounding is innocuous for division when the wider
+// format has >= 2p + 2 bits, 53 >= 50; checked exhaustively for x in [1,
+// 2^30)), and HIP's f32 division is correctly rounded (no fast math): the same
+// bits as the f64 division at a fraction of its VALU cost.
+__device__ __forceinline__ float ns_sigmoid(float e) { return 1.0f / (1.0f + e); }
+
 // ---------------------------------------------------------------------------
 // The per-target update (Word2Vec.cpp:238-246 HS; :261-268 NS), for up to
 // MAXT distinct rows at once. Lane (t0 + t) of row_l / code_l holds target t's
@@ -433,7 +442,7 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
         const float s = (float)(1.0 / (1.0 + (double)e));
         gt = (float)((1.0 - (double)code - (double)s) * (double)alpha);
       } else {
-        const float s = (float)(1.0 / (double)(1.0f + e));
+        const float s = ns_sigmoid(e);
         gt = ((float)(1 - code) - s) * alpha;
       }
       float delta[NV];
@@ -675,7 +684,7 @@ __device__ __forceinline__ void pair_update(float* M, int64_t pitch, int d, int 
                                             float (&r)[NV], const PrivRows& pr, unsigned long long* stats) {
   note_nonfinite(stats, !__builtin_isfinite(f), lane);
   const float e = expf(-f);
-  const float s = (float)(1.0 / (double)(1.0f + e));
+  const float s = ns_sigmoid(e);
   const float gt = ((float)(1 - code) - s) * alpha;
   float delta[NV];
 #pragma unroll
@@ -775,6 +784,9 @@ __device__ __forceinline__ void ns_word(const TrainArgs& a, float* M, int word, 
 // targets are applied before the next chunk's are found (a duplicate test
 // needs only the words, not the rows).
 // ---------------------------------------------------------------------------
+#ifndef W2V_MANY_NEG  // timing experiments only: 0 compiles the path out (negative >= 64 then trains wrongly)
+#define W2V_MANY_NEG 1
+#endif
 template <bool REPLAY>
 __device__ __forceinline__ int draw_chunk(const TrainArgs& a, uint32_t s, uint32_t i, int slot, int ch, int lane,
                                           const uint32_t* rp) {
@@ -898,7 +910,7 @@ __device__ __forceinline__ void sg_center(const TrainArgs& a, float* lds, const 
     if (j == i) continue;
     const int w = (j - lo < kWave) ? readlane_i(ctx_l, j - lo) : uniform_i(sent[j]);  // window > 31: span > 64
     if (HS) hs_word<NV, MAXT>(a, w, lane, x, g, alpha, cnt, lds);
-    if (NS && neg >= kWave) {
+    if (W2V_MANY_NEG && NS && neg >= kWave) {
       ns_word_many<NV, MAXT, REPLAY>(a, a.C, w, s, (uint32_t)i, slot, lane, x, g, alpha, cnt, lds, rp);
     } else if (NS) {
       const int gs = slot % G;
@@ -954,7 +966,7 @@ __device__ __forceinline__ void cbow_tail(const TrainArgs& a, float* lds, int i,
   }
   cnt.stamp(2);
   if (HS) hs_word<NV, MAXT>(a, c, lane, h, g, alpha, cnt, lds);
-  if (NS && a.negative >= kWave) {
+  if (W2V_MANY_NEG && NS && a.negative >= kWave) {
     ns_word_many<NV, MAXT, REPLAY>(a, a.W, c, s, (uint32_t)i, 0, lane, h, g, alpha, cnt, lds, rp);
   } else if (NS) {
     const int nd = a.negative;

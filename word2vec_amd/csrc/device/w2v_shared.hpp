@@ -175,11 +175,11 @@ __device__ __forceinline__ void pair_fixup(f32x4& t0, f32x4& t1, int col) {
 // wave's operations in order; this only stops the compiler reordering them).
 __device__ __forceinline__ void wave_lds_order() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
 
-// g of Word2Vec.cpp:263-264 for one (input, output) pair: f = sigma(L) through
-// double as there, g = (label - f) * alpha.
+// g of Word2Vec.cpp:263-264 for one (input, output) pair: f = sigma(L) with
+// the reference's rounding (ns_sigmoid), g = (label - f) * alpha.
 __device__ __forceinline__ float sn_grad(float l, bool positive, float alpha) {
   const float e = expf(-l);
-  const float f = (float)(1.0 / (double)(1.0f + e));
+  const float f = ns_sigmoid(e);
   return ((positive ? 1.0f : 0.0f) - f) * alpha;
 }
 
