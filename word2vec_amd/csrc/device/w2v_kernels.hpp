@@ -390,7 +390,11 @@ __device__ __forceinline__ void priv_add(const PrivRows& pr, int64_t row, int d,
 // format has >= 2p + 2 bits, 53 >= 50; checked exhaustively for x in [1,
 // 2^30)), and HIP's f32 division is correctly rounded (no fast math): the same
 // bits as the f64 division at a fraction of its VALU cost.
+#ifndef W2V_NS_SIGMOID_F64  // timing experiments only: 1 = the f64 division (same bits, more VALU)
 __device__ __forceinline__ float ns_sigmoid(float e) { return 1.0f / (1.0f + e); }
+#else
+__device__ __forceinline__ float ns_sigmoid(float e) { return (float)(1.0 / (double)(1.0f + e)); }
+#endif
 
 // ---------------------------------------------------------------------------
 // The per-target update (Word2Vec.cpp:238-246 HS; :261-268 NS), for up to
