@@ -20,15 +20,21 @@ from tests.harness import MODES, check_parity, device_config, device_from_oracle
 # build reproduces them exactly):
 #   single update (48 tokens over 400 types), north_star's 1e-5 norm-wise:
 #     measured <= 2.1e-6 except CBOW-NS's W (5.7e-5: ulp_matrices, harness);
-#     per element <= 8.5e-4 -> 2e-3
+#     per element <= 8.5e-4 -> 2e-3, CBOW-NS's W 3.4e-3 -> 5e-3 (the same
+#     last-bit roundings of a ~1e-6 update)
 #   the original single sentence (120 tokens over 60 types, every row updated
 #     dozens of times): 1e-5 norm-wise too, except CBOW-NS's W, measured
 #     2.2e-5 (its own bound, 5e-5); per element <= 1.1e-3 (SG-HS's W), CBOW-NS's
 #     W 2.1e-3 (5e-3)
 #   multi-sentence runs (epochs, widths, Philox, wide windows): measured
 #     <= 3.0e-6 norm-wise, <= 9.2e-4 per element -> 2e-5 / 2e-3
+#   round 4's lifted limits (rows of 1100 / 2048 floats, negative 64-300,
+#     window 200): measured <= 1.7e-5 norm-wise, 4.1e-3 per element (CBOW-HS's
+#     C at d 2048: 2048-term dot products, rows updated dozens of times;
+#     profiles/r04a_parity_errors.jsonl) -> 2e-5 / 5e-3
 SINGLE = (1e-5, 2e-3)
 MULTI = (2e-5, 2e-3)
+LIFTED = (2e-5, 5e-3)
 
 pytestmark = pytest.mark.gpu
 
@@ -68,7 +74,9 @@ def test_replay_single_sentence(mode, dim):
     # compounds, which is the multi-update regime below)
     sents = zipf_sentences(1, 48, 400, seed=3)
     got, want, init = _run_replay(mode, sents, dim=dim, window=5, iters=1, table_size=10_000, min_count=1)
-    check_parity(got, want, init, *SINGLE, tag=f"single {mode} d{dim}", ulp_matrices=(0,) if mode == "cbow_ns" else ())
+    cbow_ns = mode == "cbow_ns"
+    check_parity(got, want, init, *SINGLE, tag=f"single {mode} d{dim}", ulp_matrices=(0,) if cbow_ns else (),
+                 overrides={0: (SINGLE[0], 5e-3)} if cbow_ns else None)
 
 
 @pytest.mark.parametrize("mode", list(MODES))
@@ -297,7 +305,7 @@ def _philox_sequential(mode, sents, dim, window, negative, key, ts=100_000, seed
     assert st["words"] == o.current_words
     got = d.download_model()
     want = [o.matrix(k) if got[k] is not None else None for k in range(3)]
-    check_parity(got, want, init, *MULTI, tag=tag)
+    check_parity(got, want, init, *LIFTED, tag=tag)
     d.close()
     return st
 
@@ -315,7 +323,7 @@ def test_replay_many_negatives(mode, negative):
     negatives (parity at negative 100)."""
     sents = zipf_sentences(4, 150, 3000, seed=41, ragged=True)
     got, want, init = _run_replay_neg(mode, sents, negative)
-    check_parity(got, want, init, *MULTI, tag=f"replay {mode} neg{negative}")
+    check_parity(got, want, init, *LIFTED, tag=f"replay {mode} neg{negative}")
 
 
 def _run_replay_neg(mode, sents, negative, dim=48, window=5):
@@ -367,7 +375,7 @@ def test_replay_huge_window(mode):
     (parity at window 200)."""
     sents = zipf_sentences(3, 700, 300, seed=45, ragged=True)
     got, want, init = _run_replay(mode, sents, dim=48, window=200, iters=1, table_size=10_000)
-    check_parity(got, want, init, *MULTI, tag=f"huge replay {mode} w200")
+    check_parity(got, want, init, *LIFTED, tag=f"huge replay {mode} w200")
 
 
 @pytest.mark.parametrize("mode", ["sg_ns", "cbow_ns", "cbow_hs"])
@@ -382,13 +390,17 @@ def test_replay_wide_rows(mode, dim):
     """Rows past 1024 floats (24 and 32 floats per lane)."""
     sents = zipf_sentences(2, 120, 200, seed=49, ragged=True)
     got, want, init = _run_replay(mode, sents, dim=dim, window=5, iters=1, table_size=10_000)
-    check_parity(got, want, init, *MULTI, tag=f"wide rows {mode} d{dim}")
+    check_parity(got, want, init, *LIFTED, tag=f"wide rows {mode} d{dim}")
 
 
 def test_parallel_huge_window_and_many_negatives_run():
-    """The parallel schedule (many waves, the huge-window scratch per wave)
-    with window 150 and negative 80: trains, counts every word once, finite."""
-    sents = zipf_sentences(200, 400, 2000, seed=51, ragged=True)
+    """The parallel schedule with window 150 and negative 80 on 64 waves
+    (several workgroups, each wave its own slice of the huge-window scratch):
+    trains, counts every word once, stays finite. (At full concurrency on a
+    2000-word vocabulary and alpha 0.025 this configuration diverges — 300
+    contexts x 81 targets per center on a few thousand rows — which
+    w2v_dev_train_epoch reports as W2V_ERR_DIVERGED.)"""
+    sents = zipf_sentences(200, 400, 20000, seed=51, ragged=True)
     for mode in ("cbow_ns", "sg_ns"):
         o = oracle_run(sents, mode, dim=64, window=150, iters=1, table_size=100_000, train=False)
         o.build_sample()
@@ -396,10 +408,11 @@ def test_parallel_huge_window_and_many_negatives_run():
 
         m = MODES[mode]
         cfg = Config(word_dim=64, window=150, negative=80, hs=False, cbow=m["model"] == "cbow", cbow_mean=True,
-                     iter=1, init_alpha=0.025, min_alpha=2.5e-6, table_size=100_000)
+                     iter=1, init_alpha=0.0025, min_alpha=2.5e-6, table_size=100_000)
         d = device_from_oracle(o, cfg, initial=False)
         d.set_rng(N.W2V_RNG_PHILOX, 99)
         d.set_schedule(N.W2V_SCHED_PARALLEL)
+        d.set_max_waves(64)
         d.set_progress(0)
         st = d.train_epoch(0, np.random.default_rng(3).permutation(o.samples()[1].size - 1))
         ids, _ = o.samples()
