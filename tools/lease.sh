@@ -11,7 +11,7 @@
 #   profile:<cN>              tools/profile.sh (kernel trace + FETCH_SIZE + WRITE_SIZE passes) +
 #                             tools/pmc_summary.py -> profiles/<tag>_<cN>_* and profiles/pmc_traffic.json
 #   pmc:<cN>[:<passes>]       tools/pmc.sh counter passes (default sq1 sq2 tcc atom)
-#   py:<script>[:<args>]      python3 -u <script> <args> (600 s; LEASE_PY_TIMEOUT overrides)
+#   py:<script>[:<args>]      python3 -u <script> <args> (600 s; LEASE_PY_TIMEOUT overrides) -> <tag>_<step#>_<script>.log
 #   sh:<script>[:<args>]      bash <script> <args> (900 s), e.g. sh:tools/r03/ab.sh:<tag> <variant> "c3 c1" 2
 # Outputs: gpurun_out/<tag>_*; profiles written on the box come back under
 # gpurun_out/<tag>_profiles/ (copy them into profiles/ to commit).
@@ -20,7 +20,9 @@ TAG=$1; shift
 OUT=gpurun_out
 mkdir -p $OUT/${TAG}_profiles
 stop() { echo "STOP at step '$1' (rc=$2)"; exit 1; }
+n=0
 for step in "$@"; do
+  n=$((n + 1))
   IFS=: read -r kind a b <<< "$step"
   echo "== $step ($(date +%T))"
   case $kind in
@@ -46,11 +48,13 @@ for step in "$@"; do
       python tools/pmc_table.py ${TAG}_$a > $OUT/${TAG}_pmc_table_$a.log 2>&1 || true
       cat $OUT/${TAG}_pmc_table_$a.log ;;
     py)
-      timeout -k 10 ${LEASE_PY_TIMEOUT:-600} python3 -u $a $b > $OUT/${TAG}_$(basename $a .py).log 2>&1 || stop "$step" $?
-      tail -12 $OUT/${TAG}_$(basename $a .py).log ;;
+      log=$OUT/${TAG}_${n}_$(basename $a .py).log
+      timeout -k 10 ${LEASE_PY_TIMEOUT:-600} python3 -u $a $b > $log 2>&1 || stop "$step" $?
+      tail -12 $log ;;
     sh)
-      eval "timeout -k 10 900 bash $a $b" > $OUT/${TAG}_$(basename $a .sh).log 2>&1 || stop "$step" $?
-      tail -20 $OUT/${TAG}_$(basename $a .sh).log ;;
+      log=$OUT/${TAG}_${n}_$(basename $a .sh).log
+      eval "timeout -k 10 900 bash $a $b" > $log 2>&1 || stop "$step" $?
+      tail -20 $log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
