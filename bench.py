@@ -85,7 +85,7 @@ def parse():
                          "Hogwild RMW, k = k most frequent)")
     ap.add_argument("--hot-auto", type=float, nargs=2, default=[0.0, 1.0], metavar=("ROWS", "NODES"),
                     help="thresholds of the automatic hot rows (expected updates in flight of a W / C row, a node; "
-                         "rows 0 = by the vocabulary, the library default)")
+                         "rows 0 = the library default, 1)")
     ap.add_argument("--private-rows", type=int, default=-1,
                     help="hottest output rows privatised per workgroup in LDS (-1 auto, 0 off)")
     ap.add_argument("--private-rate", type=float, default=None,

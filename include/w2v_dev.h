@@ -229,8 +229,9 @@ int w2v_dev_reset_stats(w2v_dev* h);
  *    the default) = chosen per launch from the corpus statistics: the rows
  *    and nodes whose expected updates in flight (wavefronts x expected
  *    updates per center) reach the thresholds of w2v_dev_set_hot_auto
- *    (W / C rows: by the vocabulary by default, 2 when a row's average
- *    updates in flight waves x (window + 1) / V is <= 0.1, else 1; nodes: 1);
+ *    (W / C rows: 1 by default — round 3's 2 for large vocabularies cost
+ *    configs[2] a similarity point against the sequential reference;
+ *    nodes: 1);
  *    -1 = every row, 0 = none,
  *    k > 0 = the k most frequent;
  *  - the rest: plain read-modify-write (an update racing another on the same
@@ -240,8 +241,8 @@ int w2v_dev_reset_stats(w2v_dev* h);
 #define W2V_HOT_AUTO (-2)
 int w2v_dev_set_hot_rows(w2v_dev* h, int64_t hot_rows);
 /* Thresholds of the automatic hot rows: expected updates of a W / C row, of
- * a Huffman node, in flight across the chip (rows >= 0, 0 = by the
- * vocabulary (the default, see above); nodes > 0, default 1). */
+ * a Huffman node, in flight across the chip (rows >= 0, 0 = the default, 1;
+ * nodes > 0, default 1). */
 int w2v_dev_set_hot_auto(w2v_dev* h, float tau_rows, float tau_nodes);
 /* The thresholds the last parallel launch used (additive). */
 int w2v_dev_hot_tau(w2v_dev* h, float* tau_rows, float* tau_nodes);

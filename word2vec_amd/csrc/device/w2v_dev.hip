@@ -999,28 +999,22 @@ static double private_rate_for(const w2v_dev* h, int64_t count) {
 // threshold 4 for the W / C rows the planted SG-HS run collapses (analogy
 // 6 vs 89: its center rows, V = 3.4K under 8K waves, fell to plain
 // read-modify-write; profiles/r02c_*). Returns {W / C rows, nodes}.
-// The W / C threshold when hot_tau_rows is 0 (the default): by the average
-// number of a row's updates in flight, rho = waves x (window + 1) / V. A large
-// vocabulary (rho <= 0.1: configs[2] 0.066) takes 2: 1738 -> 867 atomic rows,
-// configs[2] +1.1 % (profiles/r03w_*). Threshold 4 (435 rows, +2-11 % box to
-// box: r03a_hot_tau.log, r02z_hot_tau_probe.log) was the round-3 default
-// until a planted corpus at configs[2]'s own scale (d300, V 717K, rho 0.07,
-// 3 seeds, profiles/r03w_hot_tau_headline_scale_3seeds.log) measured what it
-// costs: analogy 99.9 / 99.5 / 93.0 / 94.9 at threshold 1 / 2 / 4 / 16 —
-// the rows between 2 and 4 updates in flight do lose updates that matter.
-// A smaller vocabulary keeps 1:
-// configs[0] (rho 0.2) gains 1-2 %, the text8-like gate corpus (rho 0.5) lost
-// up to 2.6 similarity points at 4 (one seed of three at -0.9 vs the oracle,
-// r03a), and at 4 the planted SG-HS run (V = 3.4K, rho 14) collapsed: its
-// center rows fell to plain read-modify-write (analogy 6 vs 89,
-// profiles/r02c_*). The shared-negatives kernel keeps 1 (its floor of 1000
-// atomic rows decides there).
-constexpr double kHotTauLargeV = 2.0, kHotTauSmallV = 1.0, kHotRhoLargeV = 0.1;
-static double hot_tau_for(const w2v_dev* h, double waves, bool shared) {
-  if (h->hot_tau_rows > 0.0) return h->hot_tau_rows;
-  if (shared || h->V <= 0) return kHotTauSmallV;
-  const double rho = waves * ((double)h->cfg.window + 1.0) / (double)h->V;
-  return rho <= kHotRhoLargeV ? kHotTauLargeV : kHotTauSmallV;
+// The W / C threshold when hot_tau_rows is 0 (the default) is 1 for every
+// vocabulary. Round 3 used 2 for a large vocabulary (rows' average updates in
+// flight waves x (window + 1) / V <= 0.1: configs[2], 1738 -> 867 atomic rows,
+// +1.1 %); round 4's paired gate at configs[2]'s own scale (d300, V 717K,
+// the sequential oracle's golden, tests/test_gpu_quality.py, 2 seeds) put
+// threshold 2 at -1.0 / -1.2 similarity in two leases and threshold 1 at
+// +0.03 (profiles/r04b_policy_probe_c3.log), for 1.1 % of throughput
+// (96.3 vs 97.4 M words/s, alternating on one box: r04c_ab_tau.log). Higher
+// thresholds lost more (round 3: analogy 99.9 / 99.5 / 93.0 / 94.9 at 1 / 2
+// / 4 / 16, profiles/r03w_*); at 4 the planted SG-HS run (V = 3.4K) collapsed
+// (its center rows fell to plain read-modify-write: analogy 6 vs 89,
+// profiles/r02c_*). The shared-negatives kernel keeps 1 too (its floor of
+// 1000 atomic rows decides there).
+constexpr double kHotTau = 1.0;
+static double hot_tau_for(const w2v_dev* h, double, bool) {
+  return h->hot_tau_rows > 0.0 ? h->hot_tau_rows : kHotTau;
 }
 
 static std::pair<int64_t, int64_t> auto_hot(w2v_dev* h, double waves, bool shared) {

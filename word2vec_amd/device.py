@@ -220,7 +220,7 @@ class DeviceTrainer:
 
     def set_hot_auto(self, tau_rows: float = 0.0, tau_nodes: float = 1.0):
         """Thresholds of the automatic hot rows (expected updates in flight of a W / C row, of a Huffman node);
-        tau_rows 0 = by the vocabulary (the library default: 2 for large V, 1 for small)."""
+        tau_rows 0 = the library default (1)."""
         self._chk(self.lib.w2v_dev_set_hot_auto(self.h, float(tau_rows), float(tau_nodes)), "w2v_dev_set_hot_auto")
 
     def policy(self) -> dict:
