@@ -150,8 +150,11 @@ def gpu_trainer(counts, ids, soff, raw, mode, dim, negative, alpha, W0, C0, S0, 
 _ROWS, _COLS, _TOPIC, _ROLE = 50, 4, 8, 8  # planted_zipf_ids' grid
 
 
-def _chunks(n_tokens, filler, planted, seed, dev, sent_len, chunk=1 << 26):
-    """The raw ids of the corpus, chunk by chunk (deterministic in `seed`)."""
+def _chunks(n_tokens, filler, planted, seed, dev, sent_len, chunk=1 << 26, planted_sents=1.0):
+    """The raw ids of the corpus, chunk by chunk (deterministic in `seed`);
+    only a fraction `planted_sents` of the sentences carry planted words (at
+    `planted` of their positions: the relations stay dense inside windows
+    while the corpus's planted total shrinks)."""
     import torch
 
     g = torch.Generator(device=dev)
@@ -166,12 +169,16 @@ def _chunks(n_tokens, filler, planted, seed, dev, sent_len, chunk=1 << 26):
     cdf /= cdf[-1].clone()
     si = torch.randint(_ROWS, (n_sent,), generator=g, device=dev)
     sj = torch.randint(_COLS, (n_sent,), generator=g, device=dev)
+    sp = (torch.rand(n_sent, generator=g, device=dev) < planted_sents) if planted_sents < 1.0 else None
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
         m = e - s
         tok = torch.searchsorted(cdf, torch.rand(m, generator=g, device=dev, dtype=torch.float64), right=True)
         tok.clamp_(max=filler - 1)
-        pos = torch.nonzero(torch.rand(m, generator=g, device=dev) < planted).squeeze(1)
+        pick = torch.rand(m, generator=g, device=dev) < planted
+        if sp is not None:
+            pick &= sp[(torch.arange(s, e, device=dev) // sent_len)]
+        pos = torch.nonzero(pick).squeeze(1)
         k = pos.numel()
         sent = (pos + s) // sent_len
         i, j = si[sent], sj[sent]
@@ -190,7 +197,7 @@ def _chunks(n_tokens, filler, planted, seed, dev, sent_len, chunk=1 << 26):
         yield s, e, tok
 
 
-def planted_zipf_ids_torch(n_tokens, filler, planted, seed, dev, sent_len=1000):
+def planted_zipf_ids_torch(n_tokens, filler, planted, seed, dev, sent_len=1000, planted_sents=1.0):
     """planted_zipf_ids' law (Zipf(s=1) filler, the 50 x 4 planted grid) drawn
     with torch on `dev` (the GPU: 10 B tokens in seconds; not the same draws as
     the numpy generator), every rank in vocab (asserted: no OOV, so every
@@ -203,7 +210,7 @@ def planted_zipf_ids_torch(n_tokens, filler, planted, seed, dev, sent_len=1000):
     n_raw = filler + _ROWS * _COLS + _ROWS * _TOPIC + _COLS * _ROLE
     counts = torch.zeros(n_raw, dtype=torch.int64, device=dev)
     n = 0
-    for s, e, tok in _chunks(n_tokens, filler, planted, seed, dev, sent_len):
+    for s, e, tok in _chunks(n_tokens, filler, planted, seed, dev, sent_len, planted_sents=planted_sents):
         counts += torch.bincount(tok, minlength=n_raw)
         n = e
     counts_h = counts.cpu().numpy()
@@ -214,7 +221,7 @@ def planted_zipf_ids_torch(n_tokens, filler, planted, seed, dev, sent_len=1000):
     remap[order] = np.arange(n_raw, dtype=np.int32)
     remap_d = torch.from_numpy(remap).to(dev)
     ids = np.empty(n, np.int32)
-    for s, e, tok in _chunks(n_tokens, filler, planted, seed, dev, sent_len):
+    for s, e, tok in _chunks(n_tokens, filler, planted, seed, dev, sent_len, planted_sents=planted_sents):
         ids[s:e] = remap_d[tok].cpu().numpy()
     names = ([f"f{k}" for k in range(filler)] + [f"e{a}_{b}" for a in range(_ROWS) for b in range(_COLS)]
              + [f"t{a}_{k}" for a in range(_ROWS) for k in range(_TOPIC)]

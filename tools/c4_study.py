@@ -40,7 +40,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tokens", type=float, default=1e10)
     ap.add_argument("--filler", type=int, default=1_000_000)
-    ap.add_argument("--planted", type=float, default=0.001)
+    ap.add_argument("--planted", type=float, default=0.05)
+    ap.add_argument("--planted-sents", type=float, default=1.0,
+                    help="fraction of the sentences that carry planted words (at --planted of their positions)")
     ap.add_argument("--dim", type=int, default=300)
     ap.add_argument("--negative", type=int, default=5)
     ap.add_argument("--mode", default="sg_ns", choices=["sg_ns", "sg_sn"])
@@ -52,8 +54,8 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     t0 = time.time()
-    data = gen_corpus(int(args.tokens), args.filler, args.planted, args.seed, dev)
-    print(json.dumps({"corpus_tokens": data[5], "V": int(data[1].size), "planted": args.planted, "dim": args.dim,
+    data = gen_corpus(int(args.tokens), args.filler, args.planted, args.seed, dev, planted_sents=args.planted_sents)
+    print(json.dumps({"corpus_tokens": data[5], "V": int(data[1].size), "planted": args.planted, "planted_sents": args.planted_sents, "dim": args.dim,
                       "mode": args.mode, "negative": args.negative, "rounds_per_epoch": args.rounds,
                       "gen_s": round(time.time() - t0, 1)}), flush=True)
     base = None
