@@ -241,8 +241,9 @@ def train_replicas(data, R, gmode, rounds, dim=300, negative=5, mode="sg_ns", se
     handle, as on R GPUs; replica r trains the r-th contiguous 1/R of the
     shuffled sentence order as its own corpus, its counter following the
     global alpha schedule) exchanging `rounds` times per epoch in `gmode`
-    (auto = Word2Vec::replica_mode's: sum for 2, average for more; overlapped
-    as the class does), or by one replica (R = 1). mode sg_ns or sg_sn (the
+    (auto = Word2Vec::replica_mode's: sum for 2, average for more; sat<beta> =
+    W2V_GROUP_SATURATION; overlapped as the class does), or by one replica
+    (R = 1). mode sg_ns or sg_sn (the
     shared-negatives minibatch). Returns ((analogy, similarity) of W or None
     if it diverged, train seconds)."""
     import time
@@ -277,7 +278,11 @@ def train_replicas(data, R, gmode, rounds, dim=300, negative=5, mode="sg_ns", se
     g = None
     if R > 1:
         gm = ("sum" if R <= 2 else "average") if gmode == "auto" else gmode
-        g = NativeAverager([t for t, _ in reps], overlap=True, mode=gm)
+        if gm.startswith("sat"):  # sat<beta>: W2V_GROUP_SATURATION's per-row divisors
+            g = NativeAverager([t for t, _ in reps], overlap=True, mode="sum")
+            g.set_saturation(max(1, raw // R // rounds), float(gm[3:]))
+        else:
+            g = NativeAverager([t for t, _ in reps], overlap=True, mode=gm)
     torch.cuda.synchronize()
     t0 = time.time()
     glob = 0
