@@ -372,3 +372,28 @@ def test_eight_replicas_full_concurrency_quality(tmp_path):
     d = eight - one
     print(f"eight replicas (class defaults) vs one: one {one.round(2)} eight {eight.round(2)} delta {d.round(2)}")
     assert abs(d[0]) <= 1.0 and abs(d[1]) <= 1.0, (one, eight)
+
+
+@pytest.mark.parametrize("R", [2, 8])
+def test_shared_negatives_replicas_quality(R):
+    """configs[4]'s shared-negatives minibatch (d512, negative 15) under a
+    replica group (never run there): R same-device replicas, each
+    a full-concurrency shared-negatives handle on its 1/R of the sentences, in
+    the class's auto mode (sum for two, average for more) at its automatic
+    cadence (two: 64 exchanges per epoch; more: one per kAutoAverageWords = 4
+    M words of a shard: 12 here), overlapped, against one replica at equal
+    tokens on the 400 M-token planted corpus (configs[3]'s easy regime, as the
+    SG-NS gate above): within a point both ways."""
+    import torch
+
+    from tests.planted_ids import planted_zipf_ids_torch, train_replicas
+
+    dev = torch.device("cuda", 0)
+    data = planted_zipf_ids_torch(400_000_000, 200_000, 0.05, 5, dev)
+    rounds = 64 if R == 2 else max(1, min(64, (data[5] // R) // 4_000_000))
+    one, _ = train_replicas(data, 1, "auto", 1, dim=512, negative=15, mode="sg_sn", seed=5, dev=dev)
+    many, _ = train_replicas(data, R, "auto", rounds, dim=512, negative=15, mode="sg_sn", seed=5, dev=dev)
+    assert one is not None and many is not None, "diverged"
+    d = np.array(many) - np.array(one)
+    print(f"shared negatives, {R} replicas x{rounds}: one {np.round(one, 2)} many {np.round(many, 2)} delta {d.round(2)}")
+    assert abs(d[0]) <= 1.0 and abs(d[1]) <= 1.0, (one, many)

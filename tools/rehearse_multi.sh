@@ -1,0 +1,9 @@
+# Rehearse bench.py's N > 1 path on a one-GPU box: N ranks (torchrun, gloo
+# control plane) all on cuda:0 (W2V_BENCH_SHARE_GPU=1: replicas averaged by
+# torch over gloo instead of the RCCL group, which needs one rank per GPU).
+# Checks the multi-rank code path (sharding, rounds at the configs[3] cadence,
+# barriers, max-over-ranks time); the numbers are not bench lines.
+#   bash tools/rehearse_multi.sh [N] [extra bench args]
+N=${1:-2}; shift
+W2V_BENCH_SHARE_GPU=1 timeout -k 10 400 python -m torch.distributed.run --nnodes 1 --nproc-per-node $N \
+  --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus $N --steps 2 --warmup 1 --cpu-seconds 0 "$@"
