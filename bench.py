@@ -106,7 +106,7 @@ def parse():
                     help="N>1: exchange every this many in-vocab words of a shard (default: the class's automatic "
                          "cadence on configs[3], 64 exchanges per epoch of a 1.25 B-token shard)")
     ap.add_argument("--replica-mode", default="auto", choices=["auto", "sum", "average", "row_average", "adaptive"],
-                    help="N>1: how the replicas' updates combine (auto: sum for 2 ranks, average for more, "
+                    help="N>1: how the replicas' updates combine (auto: sum for 2 ranks, adaptive for more, "
                          "as Word2Vec::replica_mode; DESIGN.md §6)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N>1: average the replicas in place on the training stream instead of from a snapshot "
@@ -254,11 +254,11 @@ def main():
     if world > 1 and not share:
         uid = [group_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        rmode = args.replica_mode if args.replica_mode != "auto" else ("sum" if world <= 2 else "average")
+        rmode = args.replica_mode if args.replica_mode != "auto" else ("sum" if world <= 2 else "adaptive")
         averager = NativeAverager([tr], uid[0], world, rank, overlap=not args.no_overlap, mode=rmode)
     else:  # N = 1 (no-op) or the one-GPU rehearsal (ranks share cuda:0: RCCL needs one rank per GPU)
         averager = TorchAverager(mats, world)
-    rmode_used = (args.replica_mode if args.replica_mode != "auto" else ("sum" if world <= 2 else "average"))
+    rmode_used = (args.replica_mode if args.replica_mode != "auto" else ("sum" if world <= 2 else "adaptive"))
     if args.sync_every > 0 or world == 1:
         rounds = n_rounds(n_sent * world, world, args.sync_every)
     else:  # every rank's shard has ~ the same words: the same round count everywhere

