@@ -351,7 +351,7 @@ def main():
         out = {
             "metric": (f"trained words/sec, dim={d} " + ("CBOW" if mode["cbow"] else "SG") + ("-HS" if mode["hs"] else ("-NS" if mode["cbow"] else "NS"))
                        + (" shared-negatives minibatch" if mode.get("shared") else "")
-                       + " (per-GPU replica, RCCL model averaging for N>1)"),
+                       + " (per-GPU replica, RCCL all-reduce of the replicas' updates for N>1)"),
             "value": round(value, 1),
             "unit": "words/s",
             "n_gpus": world,
