@@ -12,7 +12,7 @@ mkdir -p "$D/obj"
 cp "$L"/obj/*.o "$D/obj/"
 pids=()
 for n in $nvs; do  # a row width, or "shared" for the shared-negatives kernel
-  if [ "$n" = shared ]; then src=w2v_shared.hip; obj=w2v_shared.o; def=; else src=w2v_inst.hip; obj=w2v_inst_nv$n.o; def=-DW2V_NV=$n; fi
+  if [ "$n" = shared ]; then src=w2v_shared.hip; obj=w2v_shared.o; def=; else src=w2v_inst.hip; obj=w2v_inst_nv$n.o; def="-DW2V_NV=$n -mllvm -amdgpu-atomic-optimizer-strategy=None"; fi
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall $flags \
     -I"$R/include" -I"$DEV" -I"$C/host" $def -c -o "$D/obj/$obj" "$DEV/$src" &
   pids+=($!)

@@ -79,6 +79,7 @@ struct Knobs {
   int64_t sn_coherent_rows = -1; // W2V_SN_COHERENT_ROWS
   int64_t sn_atomic_rows = -1;   // W2V_SN_ATOMIC_ROWS
   int scale_resident = 0;        // W2V_SCALE_RESIDENT=1: flush scales from the chip's resident workgroups, not the launch's grid
+  double priv_tail_avg = -1;     // W2V_PRIV_TAIL_AVG: private_average of the NS output rows past the 64th (0 = plain sum)
   std::string desc;              // "NAME=value ..." of the variables that were set
 };
 
@@ -97,6 +98,7 @@ static Knobs read_knobs() {
   if (const char* v = get("W2V_SN_COHERENT_ROWS")) k.sn_coherent_rows = std::max<int64_t>(0, std::atoll(v));
   if (const char* v = get("W2V_SN_ATOMIC_ROWS")) k.sn_atomic_rows = std::max<int64_t>(0, std::atoll(v));
   if (const char* v = get("W2V_SCALE_RESIDENT")) k.scale_resident = std::atoi(v) != 0;
+  if (const char* v = get("W2V_PRIV_TAIL_AVG")) k.priv_tail_avg = std::max(0.0, std::atof(v));
   return k;
 }
 
@@ -302,7 +304,9 @@ w2v::ApplyFn apply_for(const w2v_dev* h) {
   }
 }
 
-// Instantiated row widths (floats per lane): the smallest one covering d.
+// Instantiated row widths (floats per lane): the smallest one covering d
+// (w2v_kernels.hpp kFullVecs relies on it: the vectors below the next smaller
+// width are inside d in every lane).
 int pick_nv(int d) {
   const int need = (d + w2v::kWave - 1) / w2v::kWave;
   static const int widths[] = {1, 2, 3, 4, 5, 6, 8, 12, 16, 24, 32};
@@ -901,9 +905,10 @@ static void priv_scales(w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool shared) {
   const double S = a.priv_avg, win1 = (double)h->cfg.window + 1.0, neg = (double)h->cfg.negative;
   const int64_t V = h->V;
   const bool ok = h->stats_ok;
-  auto sc = [&](double m, int k) {  // without statistics: every workgroup counted (the most damping)
+  auto sc = [&](double m, int k, double avg) {  // without statistics: every workgroup counted (the most damping)
+    if (!(avg > 0.0)) return 1.0f;
     const double n = ok ? (double)G * (1.0 - std::exp(-(double)k * m)) : (double)G;
-    return (float)(1.0 / std::max(1.0, n / S));
+    return (float)(1.0 / std::max(1.0, n / avg));
   };
   auto f = [&](int64_t r) { return ok ? h->f[(size_t)r] : 0.0; };
   auto fk = [&](int64_t r) { return ok ? h->fk[(size_t)r] : 0.0; };
@@ -915,17 +920,18 @@ static void priv_scales(w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool shared) {
       for (int p = 0; p < a.priv_n; ++p) {
         const int64_t j = a.priv_lo + p;
         const double m = !nodes ? 1.0 : cbow ? h->node_fk[(size_t)j] : win1 * h->node_f[(size_t)j];
-        a.priv_sc[p] = sc(m, a.flush_every);
+        a.priv_sc[p] = sc(m, a.flush_every, S);
       }
     } else {
       for (int p = 0; p < a.priv_n; ++p) {
         const int64_t r = a.priv_lo + p;
         const double m = (shared || cbow) ? fk(r) + neg * u(r) : win1 * (f(r) + neg * u(r));
-        a.priv_sc[p] = sc(m, a.flush_every);
+        const double avg = (p >= 64 && h->knobs.priv_tail_avg >= 0.0) ? h->knobs.priv_tail_avg : S;  // experiments
+        a.priv_sc[p] = sc(m, a.flush_every, avg);
       }
     }
   }
-  for (int p = 0; p < a.ctx_n; ++p) a.ctx_sc[p] = sc(win1 * f(p), a.ctx_flush_every);
+  for (int p = 0; p < a.ctx_n; ++p) a.ctx_sc[p] = sc(win1 * f(p), a.ctx_flush_every, S);
 }
 
 // Privatised rows by update rate (private_rate mu > 0, private_rows = -1): only
@@ -1216,7 +1222,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     }
     if (P > 0) {
       a.priv_M = hs ? h->S : (h->cfg.cbow ? h->W : h->C);
-      a.priv_lo = hs ? avail - P : 0;  // HS: the P internal nodes nearest the root (V-2)
+      a.priv_lo = (int32_t)(hs ? avail - P : 0);  // HS: the P internal nodes nearest the root (V-2)
       a.priv_n = (int32_t)P;
     }
     // Auto: CBOW-HS only. It doubles CBOW-HS throughput and raises its planted-
@@ -1292,8 +1298,8 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     // similarity points below the oracle; profiles/r02s_gpu_tests.log)
     int64_t hot = hot_for((double)g_res, true).first;
     if (h->hot_rows == W2V_HOT_AUTO) hot = std::max<int64_t>(hot, std::min<int64_t>(h->V, 1000));
-    a.hot_wc = h->hot_rows == -1 ? h->V : std::min<int64_t>(h->V, std::max<int64_t>(hot, l2_rows));
-    if (h->knobs.sn_coherent_rows >= 0) a.hot_wc = std::min<int64_t>(h->V, h->knobs.sn_coherent_rows);  // experiments
+    a.hot_wc = (int32_t)(h->hot_rows == -1 ? h->V : std::min<int64_t>(h->V, std::max<int64_t>(hot, l2_rows)));
+    if (h->knobs.sn_coherent_rows >= 0) a.hot_wc = (int32_t)std::min<int64_t>(h->V, h->knobs.sn_coherent_rows);  // experiments
     a.hot_atomic = h->sched == W2V_SCHED_PARALLEL ? hot : 0;
     if (h->knobs.sn_atomic_rows >= 0) a.hot_atomic = std::min<int64_t>(h->V, h->knobs.sn_atomic_rows);  // experiments
     priv_scales(h, a, h->knobs.scale_resident ? g_res : g, true);
@@ -1334,8 +1340,8 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     // (measured: two replicas on one GPU trained in 1/8-epoch slices collapsed
     // to analogy 3 with the launch-grid count; tests/test_gpu_replicas.py).
     const std::pair<int64_t, int64_t> hot = hot_for((double)resident_waves, false);
-    a.hot_wc = hot.first;
-    a.hot_s = (h->V - 1) - hot.second;  // the `nodes` internal nodes nearest the root (the root is V-2)
+    a.hot_wc = (int32_t)hot.first;
+    a.hot_s = (int32_t)((h->V - 1) - hot.second);  // the `nodes` internal nodes nearest the root (the root is V-2)
     h->last_hot_rows = hot.first;
     h->last_hot_nodes = h->cfg.hs ? hot.second : 0;
     h->last_priv = a.priv_n;

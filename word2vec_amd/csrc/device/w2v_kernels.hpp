@@ -100,11 +100,14 @@ struct TrainArgs {
   unsigned long long* stats;   // centers, contexts, targets, draws, sentences
   uint32_t key0, key1, epoch;
   float fixed_alpha;           // > 0: use instead of the schedule
-  int64_t hot_wc;              // W / C rows [0, hot_wc) update with atomics (shared-negatives: sc1 traffic)
-  int64_t hot_s;               // synapses1 rows [hot_s, V-1) update with atomics
+  // Row bounds are 32-bit (ids are int32): a row index read back from a lane
+  // sits in an SGPR, and gfx950's scalar unit compares 32-bit values only
+  // (64-bit bounds moved every hot / private test onto the VALU).
+  int32_t hot_wc;              // W / C rows [0, hot_wc) update with atomics (shared-negatives: sc1 traffic)
+  int32_t hot_s;               // synapses1 rows [hot_s, V-1) update with atomics
   int32_t strict;              // 1: drain own atomics before re-reading (sequential schedule)
   const float* priv_M;         // output matrix whose hottest rows are privatised in LDS (or null)
-  int64_t priv_lo;             // privatised rows [priv_lo, priv_lo + priv_n)
+  int32_t priv_lo;             // privatised rows [priv_lo, priv_lo + priv_n)
   int32_t priv_n;
   float priv_avg;              // > 0: average, not sum, the workgroups' deltas of a privatised row (see flush_private)
   int32_t flush_every;         // the privatised deltas are flushed every this many centers of the workgroup
@@ -236,10 +239,10 @@ struct PrivRows {  // one privatised row range [lo, lo + n) of matrix M (n == 0:
   float* delta = nullptr;
   unsigned long long* dirty = nullptr;
   float* M = nullptr;
-  int64_t lo = 0;
+  int lo = 0;
   int n = 0;
   bool ctx = false;  // the context range (flush scales a.ctx_sc) or the output range (a.priv_sc)
-  __device__ bool has(int64_t row) const { return row >= lo && row < lo + n; }
+  __device__ bool has(int row) const { return (unsigned)(row - lo) < (unsigned)n; }  // one scalar compare
 };
 
 template <int NV>
@@ -338,13 +341,20 @@ __device__ __forceinline__ void store_row(float* M, int64_t row, int64_t pitch, 
 // destination register (nothing to zero-fill, no wait), and a memory-side add
 // of 0 would still cost the atomic unit a request (d 300: 320 adds per row
 // instead of 300; measured 2.5 % of configs[2], profiles/r03d_guards_ab.log).
+// Vectors of a row every lane of which is inside word_dim: pick_nv
+// (w2v_dev.hip) takes the smallest row width >= ceil(d / 64) of {1, 2, 3, 4,
+// 5, 6, 8, 12, 16, 24, 32}, so d > 64 x the next smaller width and those
+// vectors need no lane mask (a mask is an exec-mask round trip per atomic).
+template <int NV>
+constexpr int kFullVecs = NV <= 6 ? NV - 1 : NV == 8 ? 6 : NV == 12 ? 8 : NV == 16 ? 12 : NV == 24 ? 16 : 24;
+
 template <int NV>
 __device__ __forceinline__ void atomic_add_row(float* M, int64_t row, int64_t pitch, int d, int lane,
                                                const float (&delta)[NV]) {
   float* p = M + row * pitch + lane;
 #pragma unroll
   for (int v = 0; v < NV; ++v)
-    if (lane + kWave * v < d)
+    if (v < kFullVecs<NV> || lane + kWave * v < d)
       (void)__hip_atomic_fetch_add(p + kWave * v, delta[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -379,7 +389,7 @@ __device__ __forceinline__ void priv_add(const PrivRows& pr, int64_t row, int d,
   float* q = pr.delta + p * (NV * kWave) + lane;
 #pragma unroll
   for (int v = 0; v < NV; ++v)
-    if (lane + kWave * v < d) atomicAdd(q + kWave * v, delta[v]);
+    if (v < kFullVecs<NV> || lane + kWave * v < d) atomicAdd(q + kWave * v, delta[v]);
   if (lane == 0) atomicOr(pr.dirty + (p >> 6), 1ull << (p & 63));
 }
 
@@ -402,6 +412,16 @@ __device__ __forceinline__ float ns_sigmoid(float e) { return (float)(1.0 / (dou
 // one per target (the same operations on the same values: bit-identical);
 // code_l holds target t's code (HS: the Huffman code; NS: 1 - label) in lane
 // c0 + t. Returns g in lane t (read back with readlane_f).
+template <bool HSF>
+__device__ __forceinline__ float grad_of(float fl, int cl, float alpha) {
+  const float e = expf(-fl);
+  if (HSF) {
+    const float s = (float)(1.0 / (1.0 + (double)e));
+    return (float)((1.0 - (double)cl - (double)s) * (double)alpha);
+  }
+  return ((float)(1 - cl) - ns_sigmoid(e)) * alpha;
+}
+
 template <int N, bool HSF>
 __device__ __forceinline__ float batch_grad(const float (&f)[N], int T, int code_l, int c0, float alpha, int lane) {
   float fl = 0.f;
@@ -414,12 +434,101 @@ __device__ __forceinline__ float batch_grad(const float (&f)[N], int T, int code
       cl = (lane == t) ? c : cl;
     }
   }
-  const float e = expf(-fl);
-  if (HSF) {
-    const float s = (float)(1.0 / (1.0 + (double)e));
-    return (float)((1.0 - (double)cl - (double)s) * (double)alpha);
+  return grad_of<HSF>(fl, cl, alpha);
+}
+
+// ---------------------------------------------------------------------------
+// The dot products of a batch of targets, reduced together (W2V_BATCH_DOTS).
+// One wave_sum per target costs 6 DPP adds + a readlane each, and the batch's
+// sigma step then gathers the sums back into lanes (2 selects + a readlane per
+// target): ~13 VALU per target on a kernel that at d = 100 keeps the VALU busy
+// ~77 % of its cycles (profiles/r04c_c1_pmc_counters.json: SQ_ACTIVE_INST_VALU
+// / SQ_WAVE_CYCLES per SIMD). Instead the NB (4 or 8) per-lane partials are
+// folded pairwise, halving the vector count at each step:
+//   xor 32  v_permlane32_swap(a, b): a = [a.lo | b.lo], b = [a.hi | b.hi];
+//           a + b holds a's half-sums in lanes 0-31 and b's in lanes 32-63
+//   xor 16  v_permlane16_swap (odd rows of the first operand with even rows
+//           of the second): rows of a + b = [a, b, a', b'] sums
+//   xor 8   keep / give selected by lane bit 3 plus a row_ror:8 DPP add
+//   xor 4, 2, 1 (one vector left): quad_perm and row_half_mirror DPP adds
+// so each group of 8 lanes (NB = 4: of 16) ends with one target's total:
+// 18 VALU for 8 targets instead of ~104. The lanes of a group hold identical
+// bits (a + b == b + a). Only the order of the 64-term sum changes.
+// ---------------------------------------------------------------------------
+#ifndef W2V_BATCH_DOTS
+#define W2V_BATCH_DOTS 1
+#endif
+__device__ __forceinline__ void swap32(float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void swap16(float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+// 16-lane row r of a permlane16-folded vector holds pair member
+// ((r & 1) << 1) | (r >> 1) (rows 0..3: members 0, 2, 1, 3; an involution).
+__host__ __device__ constexpr int row_member(int r) { return ((r & 1) << 1) | (r >> 1); }
+template <int N>
+constexpr int kBatchN = N <= 4 ? 4 : 8;
+// The first lane of target t's group after batch_dots<N>.
+template <int N>
+__device__ __forceinline__ constexpr int batch_lane(int t) {
+  return kBatchN<N> == 8 ? 16 * row_member(t & 3) + 8 * (t >> 2) : 16 * row_member(t);
+}
+// The target whose total lane `lane` holds after batch_dots<N>.
+template <int N>
+__device__ __forceinline__ int batch_target(int lane) {
+  return kBatchN<N> == 8 ? 4 * ((lane >> 3) & 1) + row_member(lane >> 4) : row_member(lane >> 4);
+}
+
+template <int N>
+__device__ __forceinline__ float batch_dots(const float (&p)[N], int lane) {
+  static_assert(N >= 1 && N <= 8, "batch of 1..8 targets");
+  constexpr int NB = kBatchN<N>;
+  float q[NB / 2];
+#pragma unroll
+  for (int k = 0; k < NB / 2; ++k) {  // xor 32
+    float a = 2 * k < N ? p[2 * k] : 0.f, b = 2 * k + 1 < N ? p[2 * k + 1] : 0.f;
+    swap32(a, b);
+    q[k] = a + b;
   }
-  return ((float)(1 - cl) - ns_sigmoid(e)) * alpha;
+  float r[NB / 4];
+#pragma unroll
+  for (int k = 0; k < NB / 4; ++k) {  // xor 16
+    float a = q[2 * k], b = q[2 * k + 1];
+    swap16(a, b);
+    r[k] = a + b;
+  }
+  float v;
+  if (NB == 8) {  // xor 8: lanes with bit 3 clear keep r[0], set keep r[NB / 4 - 1]
+    const bool hi = (lane & 8) != 0;
+    const float keep = hi ? r[NB / 4 - 1] : r[0], give = hi ? r[0] : r[NB / 4 - 1];
+    v = keep + dpp_f<0x128>(give);  // row_ror:8 (a lane 8 apart: the other bit-3 half)
+  } else {
+    v = r[0] + dpp_f<0x128>(r[0]);
+  }
+  v += dpp_f<0xb1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4e>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);  // row_half_mirror: the other quad of the 8
+  return v;
+}
+
+// batch_grad over batch_dots' layout: lane L evaluates target batch_target(L)
+// (its code fetched with one permute); counts the batch's non-finite scores.
+template <int N, bool HSF>
+__device__ __forceinline__ float batch_grad_l(float fl, int T, int code_l, int c0, float alpha, int lane,
+                                              unsigned long long* stats) {
+  const int t = batch_target<N>(lane);
+  const int cl = __shfl(code_l, (c0 + t) & (kWave - 1));
+  if (stats) {
+    constexpr int grp = kBatchN<N> == 8 ? 7 : 15;
+    const unsigned long long bad = ballot(t < T && (lane & grp) == 0 && !__builtin_isfinite(fl));
+    if (bad && lane == 0) atomicAdd(stats + kNonFinite, (unsigned long long)__popcll(bad));
+  }
+  return grad_of<HSF>(fl, cl, alpha);
 }
 
 __device__ __forceinline__ float readlane_f(float v, int l) {
@@ -454,6 +563,19 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
       priv_read<NV>(pr, rows[t], lane, r[t]);
     }
   }
+#if W2V_BATCH_DOTS
+  float pd[MAXT];
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    pd[t] = 0.f;
+    if (t < T) {  // the first product starts the sum (0 + p would cost an add per target)
+      pd[t] = r[t][0] * x[0];
+#pragma unroll
+      for (int v = 1; v < NV; ++v) pd[t] += r[t][v] * x[v];
+    }
+  }
+  const float g_l = batch_grad_l<MAXT, HSF>(batch_dots<MAXT>(pd, lane), T, code_l, t0, alpha, lane, stats);
+#else
   float f[MAXT];
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) {
@@ -466,11 +588,16 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
     }
   }
   const float g_l = batch_grad<MAXT, HSF>(f, T, code_l, t0, alpha, lane);
+#endif
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) {
     if (t < T) {
+#if W2V_BATCH_DOTS
+      const float gt = readlane_f(g_l, batch_lane<MAXT>(t));
+#else
       if (stats) note_nonfinite(stats, !__builtin_isfinite(f[t]), lane);
       const float gt = readlane_f(g_l, t);
+#endif
       float delta[NV];
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
@@ -563,6 +690,19 @@ __device__ __forceinline__ void hs_score(const TrainArgs& a, int T, int row_l, i
       const int row = readlane_i(row_l, t0 + t);
       if (pr.has(row)) priv_read<NV>(pr, row, lane, r[t]);
     }
+#if W2V_BATCH_DOTS
+  float pd[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    pd[t] = 0.f;
+    if (t < T) {  // the first product starts the sum (0 + p would cost an add per target)
+      pd[t] = r[t][0] * x[0];
+#pragma unroll
+      for (int v = 1; v < NV; ++v) pd[t] += r[t][v] * x[v];
+    }
+  }
+  const float g_l = batch_grad_l<MT, true>(batch_dots<MT>(pd, lane), T, code_l, t0, alpha, lane, a.stats);
+#else
   float f[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) {
@@ -575,12 +715,17 @@ __device__ __forceinline__ void hs_score(const TrainArgs& a, int T, int row_l, i
     }
   }
   const float g_l = batch_grad<MT, true>(f, T, code_l, t0, alpha, lane);
+#endif
 #pragma unroll
   for (int t = 0; t < MT; ++t) {
     gt[t] = 0.f;
     if (t < T) {
+#if W2V_BATCH_DOTS
+      gt[t] = readlane_f(g_l, batch_lane<MT>(t));
+#else
       note_nonfinite(a.stats, !__builtin_isfinite(f[t]), lane);
       gt[t] = readlane_f(g_l, t);
+#endif
 #pragma unroll
       for (int v = 0; v < NV; ++v) g[v] += gt[t] * r[t][v];
     }
@@ -657,17 +802,14 @@ __device__ __forceinline__ int ns_targets(int neg, int word, int negw_l, int bas
     const int v = readlane_i(nk, j);
     dup = dup || (lane > j && nk == v);
   }
-  unsigned long long uniq = ballot(!dup);
-  tgt_l = (lane == 0) ? word : 0;
-  int m = 1;
-  while (uniq) {
-    const int b = __builtin_ctzll(uniq);
-    uniq &= uniq - 1;
-    const int v = readlane_i(nk, b);
-    if (lane == m) tgt_l = v;
-    ++m;
-  }
-  return m;
+  const unsigned long long uniq = ballot(!dup);
+  // compaction in one forward permute: the k-th unique draw (in lane order)
+  // goes to lane 1 + k; duplicates to lane 0, which then takes the positive
+  // (a walk over the set bits cost ~4 VALU + 6 SALU per target)
+  const int k = __builtin_amdgcn_mbcnt_hi((unsigned)(uniq >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)uniq, 0u));
+  const int v = __builtin_amdgcn_ds_permute((dup ? 0 : 1 + k) << 2, nk);
+  tgt_l = (lane == 0) ? word : v;
+  return 1 + __popcll(uniq);
 }
 
 // The T targets of tgt_l / code_l, MAXT rows per batch.
