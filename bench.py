@@ -111,11 +111,10 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true",
                     help="N>1: average the replicas in place on the training stream instead of from a snapshot "
                          "on a communication stream overlapped with the next round")
-    args = ap.parse_args()
-    if args.config:
-        for k, v in CONFIGS[args.config].items():
-            setattr(args, k, v)
-    return args
+    pre, _ = ap.parse_known_args()
+    if pre.config:  # the preset's values are defaults: flags given explicitly still win (e.g. --mode)
+        ap.set_defaults(**CONFIGS[pre.config])
+    return ap.parse_args()
 
 
 def log(*a):
