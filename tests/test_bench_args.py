@@ -1,0 +1,31 @@
+"""bench.py's argument handling (CPU only): a BASELINE preset (--config) sets
+defaults, and flags given explicitly win over it (DESIGN.md §4.1's per-mode
+table runs `--config c3 --mode cbow_hs`)."""
+import importlib.util
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _parse(argv, monkeypatch):
+    spec = importlib.util.spec_from_file_location("bench_under_test", ROOT / "bench.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    monkeypatch.setattr(sys, "argv", ["bench.py", *argv])
+    return mod.parse()
+
+
+def test_preset_sets_defaults(monkeypatch):
+    a = _parse(["--config", "c1"], monkeypatch)
+    assert (a.mode, a.dim, a.negative, a.vocab, a.tokens) == ("sg_ns", 100, 5, 350_000, 17_000_000)
+
+
+def test_explicit_flags_override_preset(monkeypatch):
+    a = _parse(["--config", "c3", "--mode", "cbow_hs", "--dim", "200"], monkeypatch)
+    assert (a.mode, a.dim, a.vocab, a.tokens) == ("cbow_hs", 200, 1_000_000, 50_000_000)
+
+
+def test_no_preset_is_the_headline(monkeypatch):
+    a = _parse([], monkeypatch)
+    assert (a.mode, a.dim, a.negative, a.gpus) == ("sg_ns", 300, 5, 1)
