@@ -38,12 +38,28 @@ MODES = {
     "sg_sn": dict(cbow=False, hs=False, shared=True),
 }
 MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X dense f32-input MFMA (MI355X_MICROARCH.md)
-# configs[3] (10 B tokens on 8 GPUs) under Word2Vec::sync_words = 0 (the class's
-# automatic cadence, 64 exchanges per epoch: Word2Vec.cpp kAutoReplicaRounds):
-# one exchange per 10e9 / 8 / 64 words of a replica's shard. bench.py --gpus N
-# is configs[3]'s per-GPU step, so it exchanges at that cadence (3 exchanges per
-# 50 M-token step) — what the product runs on that workload.
-CONFIG3_SYNC_WORDS = 10_000_000_000 // 8 // 64
+# configs[3] (10 B tokens over N GPUs) under Word2Vec::sync_words = 0 (the
+# class's automatic cadence, 64 exchanges per epoch: Word2Vec.cpp
+# kAutoReplicaRounds): one exchange per 10e9 / N / 64 words of a replica's
+# shard, in the class's auto mode for that shard (Word2Vec::replica_mode: the
+# mean for N <= 4 — 2.5-5 B-word shards —, the adaptive divisor for more).
+# bench.py --gpus N is configs[3]'s per-GPU step, so it exchanges at that
+# cadence and in that mode — what the product runs on that workload.
+CONFIG3_TOKENS = 10_000_000_000
+AUTO_ROUNDS, AUTO_AVERAGE_WORDS, AUTO_AVERAGE_REPLICAS = 64, 4_000_000, 4  # include/Word2Vec.h
+
+
+def config3_sync_words(world):
+    return CONFIG3_TOKENS // max(1, world) // AUTO_ROUNDS
+
+
+def auto_replica_mode(world, shard_words=None):
+    """Word2Vec::replica_mode auto (Word2Vec.cpp run_epochs_replicas) for
+    `world` replicas of configs[3]'s shards (or shards of `shard_words`)."""
+    shard = CONFIG3_TOKENS // max(1, world) if shard_words is None else shard_words
+    if world <= AUTO_AVERAGE_REPLICAS and shard >= AUTO_ROUNDS * AUTO_AVERAGE_WORDS:
+        return "average"
+    return "sum" if world <= 2 else "adaptive"
 
 # BASELINE.json configs on this bench's synthetic Zipf corpora (text8 and the
 # 1B-Word corpus are not available offline): --config cN sets these fields.
@@ -64,7 +80,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", choices=list(CONFIGS), default=None,
-                    help="BASELINE.json config preset (overrides --mode/--dim/--negative/--vocab/--tokens)")
+                    help="BASELINE.json config preset (the defaults of --mode/--dim/--negative/--vocab/--tokens/...)")
     ap.add_argument("--mode", default="sg_ns", choices=list(MODES))
     ap.add_argument("--dim", type=int, default=300)
     ap.add_argument("--negative", type=int, default=5)
@@ -102,12 +118,12 @@ def parse():
                     help="N=1 only: let the library allocate the matrices instead of torch")
     ap.add_argument("--sync-every", type=int, default=0,
                     help="N>1: exchange every this many sentences of a shard (0 = by --sync-words)")
-    ap.add_argument("--sync-words", type=int, default=CONFIG3_SYNC_WORDS,
-                    help="N>1: exchange every this many in-vocab words of a shard (default: the class's automatic "
-                         "cadence on configs[3], 64 exchanges per epoch of a 1.25 B-token shard)")
+    ap.add_argument("--sync-words", type=int, default=0,
+                    help="N>1: exchange every this many in-vocab words of a shard (0: the class's automatic "
+                         "cadence on configs[3], 64 exchanges per epoch of a 10 B / N-token shard)")
     ap.add_argument("--replica-mode", default="auto", choices=["auto", "sum", "average", "row_average", "adaptive"],
-                    help="N>1: how the replicas' updates combine (auto: sum for 2 ranks, adaptive for more, "
-                         "as Word2Vec::replica_mode; DESIGN.md §6)")
+                    help="N>1: how the replicas' updates combine (auto: as Word2Vec::replica_mode on configs[3]'s "
+                         "shards: average for <= 4 ranks, adaptive for more; DESIGN.md §6.2)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N>1: average the replicas in place on the training stream instead of from a snapshot "
                          "on a communication stream overlapped with the next round")
@@ -253,15 +269,15 @@ def main():
     if world > 1 and not share:
         uid = [group_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        rmode = args.replica_mode if args.replica_mode != "auto" else ("sum" if world <= 2 else "adaptive")
+        rmode = args.replica_mode if args.replica_mode != "auto" else auto_replica_mode(world)
         averager = NativeAverager([tr], uid[0], world, rank, overlap=not args.no_overlap, mode=rmode)
     else:  # N = 1 (no-op) or the one-GPU rehearsal (ranks share cuda:0: RCCL needs one rank per GPU)
         averager = TorchAverager(mats, world)
-    rmode_used = (args.replica_mode if args.replica_mode != "auto" else ("sum" if world <= 2 else "adaptive"))
+    rmode_used = args.replica_mode if args.replica_mode != "auto" else auto_replica_mode(world)
     if args.sync_every > 0 or world == 1:
         rounds = n_rounds(n_sent * world, world, args.sync_every)
     else:  # every rank's shard has ~ the same words: the same round count everywhere
-        rounds = max(1, -(-int(ids_h.size) // max(1, args.sync_words)))
+        rounds = max(1, -(-int(ids_h.size) // max(1, args.sync_words or config3_sync_words(world))))
     order_dev = torch.arange(n_sent, dtype=torch.int64, device=dev)  # this rank's shard, in order
     round_words = global_round_words(local_round_words(soff_h, range(n_sent), rounds), world)
     progress = 0

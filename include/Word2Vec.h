@@ -155,11 +155,15 @@ class Word2Vec {
   // kAutoReplicaRounds exchanges per epoch; with W2V_GROUP_AVERAGE at most one
   // per kAutoAverageWords words of a shard), overlapped with the next round's
   // training unless overlap_average is false. replica_mode: a W2V_GROUP_*
-  // mode, or -1 = auto: W2V_GROUP_SUM for two replicas, W2V_GROUP_ADAPTIVE for
-  // more (the mean of a row the replicas moved alike, the sum of independent
-  // moves: summing R >= 3 replicas' updates overshoots the frequent rows
-  // R-fold and diverges, plain averaging loses the rare rows' progress;
-  // DESIGN.md §6 has the measured tables). Empty = one device (gpu_device).
+  // mode, or -1 = auto: W2V_GROUP_AVERAGE for up to kAutoAverageReplicas
+  // replicas whose shards hold >= kAutoReplicaRounds x kAutoAverageWords words
+  // (configs[3]'s scale: there the sum and the adaptive divisor lose 10-36
+  // analogy points at two and four replicas); otherwise W2V_GROUP_SUM for two
+  // replicas, W2V_GROUP_ADAPTIVE for more (the mean of a row the replicas
+  // moved alike, the sum of independent moves: summing R >= 3 replicas'
+  // updates overshoots the frequent rows R-fold and diverges, plain averaging
+  // of short shards loses the rare rows' progress; DESIGN.md §6 has the
+  // measured tables). Empty = one device (gpu_device).
   std::vector<int> gpu_devices;
   int64_t sync_words = 0;
   bool overlap_average = true;
@@ -169,6 +173,8 @@ class Word2Vec {
   // per this many words of a shard, so each round's mean spans rows every
   // replica trained
   static const int64_t kAutoAverageWords = 4000000;
+  // replica_mode auto averages at most this many replicas
+  static const int64_t kAutoAverageReplicas = 4;
   bool verbose = true;       // progress line per epoch (the reference prints one
                              // every 100 sentences, Word2Vec.cpp:382-386)
   // Train on a corpus that is already token ids (no strings): ids index

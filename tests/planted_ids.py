@@ -241,7 +241,7 @@ def train_replicas(data, R, gmode, rounds, dim=300, negative=5, mode="sg_ns", se
     handle, as on R GPUs; replica r trains the r-th contiguous 1/R of the
     shuffled sentence order as its own corpus, its counter following the
     global alpha schedule) exchanging `rounds` times per epoch in `gmode`
-    (auto = Word2Vec::replica_mode's: sum for 2, adaptive for more; sat<beta> =
+    (auto = Word2Vec::replica_mode's: average for <= 4 replicas of long shards, else sum for 2, adaptive for more; sat<beta> =
     W2V_GROUP_SATURATION; overlapped as the class does), or by one replica
     (R = 1). mode sg_ns or sg_sn (the
     shared-negatives minibatch). Returns ((analogy, similarity) of W or None
@@ -277,7 +277,10 @@ def train_replicas(data, R, gmode, rounds, dim=300, negative=5, mode="sg_ns", se
     del W0, C0
     g = None
     if R > 1:
-        gm = ("sum" if R <= 2 else "adaptive") if gmode == "auto" else gmode
+        # auto = Word2Vec::replica_mode (Word2Vec.cpp run_epochs_replicas): the mean for <= 4 replicas of
+        # >= 64 x 4 M-word shards, else the sum for two, the adaptive divisor for more
+        gm = (("average" if R <= 4 and raw // R >= 64 * 4_000_000 else "sum" if R <= 2 else "adaptive")
+              if gmode == "auto" else gmode)
         if gm.startswith("sat"):  # sat<beta>: W2V_GROUP_SATURATION's per-row divisors
             g = NativeAverager([t for t, _ in reps], overlap=True, mode="sum")
             g.set_saturation(max(1, raw // R // rounds), float(gm[3:]))

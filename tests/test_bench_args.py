@@ -29,3 +29,18 @@ def test_explicit_flags_override_preset(monkeypatch):
 def test_no_preset_is_the_headline(monkeypatch):
     a = _parse([], monkeypatch)
     assert (a.mode, a.dim, a.negative, a.gpus) == ("sg_ns", 300, 5, 1)
+
+
+def test_replica_auto_matches_the_class(monkeypatch):
+    """bench.py --gpus N exchanges like Word2Vec::replica_mode auto on
+    configs[3]'s 10 B / N-token shards (Word2Vec.cpp run_epochs_replicas)."""
+    spec = importlib.util.spec_from_file_location("bench_under_test", ROOT / "bench.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert [mod.auto_replica_mode(n) for n in (2, 4, 8)] == ["average", "average", "adaptive"]
+    assert mod.auto_replica_mode(2, 200_000_000) == "sum"  # short shards: the sum for two
+    assert mod.auto_replica_mode(3, 200_000_000) == "adaptive"
+    assert mod.config3_sync_words(8) == 10_000_000_000 // 8 // 64
+    hdr = (ROOT / "include" / "Word2Vec.h").read_text()
+    assert "kAutoReplicaRounds = 64;" in hdr and "kAutoAverageWords = 4000000;" in hdr
+    assert "kAutoAverageReplicas = 4;" in hdr

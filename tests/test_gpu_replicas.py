@@ -295,7 +295,7 @@ REPLICA_BOUND = {"cbow_hs": 1.0, "sg_ns": 1.0}
 def test_two_replicas_one_gpu_quality(mode):
     """SURVEY.md §4 level 4 through the C++ class (gpu_devices = {0, 0}) with
     the class's default exchange settings (replica_mode auto = sum for two
-    replicas, sync_words 0 = 64 exchanges per epoch): two replicas, each
+    replicas of short shards, sync_words 0 = 64 exchanges per epoch): two replicas, each
     training half of every epoch's sentences on one wavefront (the
     deterministic schedule: what is measured is the exchange, not the Hogwild
     policy), against one replica training all of them, at equal tokens
@@ -380,7 +380,7 @@ def test_shared_negatives_replicas_quality(R):
     """configs[4]'s shared-negatives minibatch (d512, negative 15) under a
     replica group (never run there): R same-device replicas, each
     a full-concurrency shared-negatives handle on its 1/R of the sentences, in
-    the class's auto mode (sum for two, adaptive for more) at its automatic
+    the class's auto mode (at 400 M tokens: sum for two, adaptive for more) at its automatic
     cadence (64 exchanges per epoch), overlapped, against one replica at equal
     tokens on the 400 M-token planted corpus (configs[3]'s easy regime, as the
     SG-NS gate above): within a point both ways."""

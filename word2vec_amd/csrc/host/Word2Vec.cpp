@@ -560,11 +560,19 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
     }
     check(w2v_group_create(reps.data(), (int32_t)R, nullptr, (int32_t)R, 0, &grp), "w2v_group_create");
     check(w2v_group_set_overlap(grp, overlap_average ? 1 : 0), "w2v_group_set_overlap");
-    // auto: the sum for two replicas; for more, the adaptive per-row divisor
-    // (the mean where the replicas moved a row alike, the sum where their
-    // moves were independent): at configs[3]'s scale it holds the single
-    // model's similarity where the plain mean loses 2.4 points
-    const int mode = replica_mode >= 0 ? replica_mode : (R <= 2 ? W2V_GROUP_SUM : W2V_GROUP_ADAPTIVE);
+    // auto: for up to kAutoAverageReplicas replicas whose
+    // shards give the averaging cadence its full kAutoReplicaRounds rounds
+    // (>= kAutoAverageWords words each), the plain mean — at 10 B tokens two
+    // and four averaged replicas hold the single model (+6.7 / +7.1 analogy,
+    // 0.0 similarity) where the sum and the adaptive divisor lose 36 and 10
+    // points; otherwise the sum for two replicas and, for more, the adaptive
+    // per-row divisor (the mean where the replicas moved a row alike, the sum
+    // where their moves were independent: at 10 B tokens eight replicas hold
+    // the single model's similarity where the plain mean loses 2.4 points)
+    const bool long_shards = train_words / (int64_t)R >= kAutoReplicaRounds * kAutoAverageWords;
+    const int mode = replica_mode >= 0 ? replica_mode
+                     : (R <= (size_t)kAutoAverageReplicas && long_shards) ? W2V_GROUP_AVERAGE
+                     : R <= 2 ? W2V_GROUP_SUM : W2V_GROUP_ADAPTIVE;
     const int64_t auto_rounds = kAutoReplicaRounds;
     check(w2v_group_set_mode(grp, mode), "w2v_group_set_mode");
     std::vector<long> sample_idx((size_t)n);

@@ -45,7 +45,7 @@ void usage() {
                "                        (default 0: 64 exchanges per epoch)\n"
                "  -overlap <0|1>        overlap the averaging with the next round's training (default 1)\n"
                "  -replica-mode <auto|sum|average|row_average|adaptive> how the replicas' updates combine\n"
-               "                        (default auto: sum for 2 replicas, adaptive for more)\n"
+               "                        (default auto: average for <= 4 replicas of >= 256 M words each, else sum for 2, adaptive for more)\n"
                "  -gpu-ingest <0|1>     count and map the corpus on the GPU (default 0: host threads)\n\n"
                "example: ./word2vec -train text8 -output vec.txt -size 300 -window 5 -subsample 1e-4 "
                "-negative 5 -model sg -train_method ns -iter 3\n";

@@ -15,10 +15,11 @@ the mean), "row_average" (per row, the mean over the replicas that changed
 it), "adaptive", or the per-row divisors of set_split / set_saturation;
 optionally overlapped with the next round's training). The constructor's
 default is "sum" with overlap off (the primitive, as the tests drive it);
-bench.py and Word2Vec::replica_mode pick "auto": sum for two replicas,
-adaptive for more (summing R >= 3 replicas diverges on the frequent rows,
-plain averaging loses the rare rows' progress;
-measured table in DESIGN.md §6), with the exchange overlapped.
+bench.py and Word2Vec::replica_mode pick "auto": the mean for up to four
+replicas of long shards (>= 64 x 4 M words: configs[3]'s scale), else the sum
+for two replicas and adaptive for more (summing R >= 3 replicas diverges on
+the frequent rows, plain averaging of short shards loses the rare rows'
+progress; measured tables in DESIGN.md §6), with the exchange overlapped.
 `TorchAverager` (model averaging
 over torch.distributed) is what the CPU tests run on the gloo backend to
 exercise the round logic, which is the same object code.
