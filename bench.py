@@ -161,8 +161,8 @@ def main():
     from word2vec_amd import _native as N
     from word2vec_amd import host
     from word2vec_amd.device import Config, DeviceTrainer
-    from word2vec_amd.replicas import (NativeAverager, TorchAverager, global_round_words, group_unique_id,
-                                       local_round_words, n_rounds, train_rounds)
+    from word2vec_amd.replicas import (global_round_words, local_round_words, make_averager, n_rounds,
+                                       train_rounds)
 
     mode = MODES[args.mode]
     neg = 0 if mode["hs"] else args.negative
@@ -266,14 +266,10 @@ def main():
     mats = [m for m in (W, Cm, S) if m is not None]
     if not mats:
         assert world == 1
-    if world > 1 and not share:
-        uid = [group_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        rmode = args.replica_mode if args.replica_mode != "auto" else auto_replica_mode(world)
-        averager = NativeAverager([tr], uid[0], world, rank, overlap=not args.no_overlap, mode=rmode)
-    else:  # N = 1 (no-op) or the one-GPU rehearsal (ranks share cuda:0: RCCL needs one rank per GPU)
-        averager = TorchAverager(mats, world)
-    rmode_used = args.replica_mode if args.replica_mode != "auto" else auto_replica_mode(world)
+    # N = 1: no-op; one rank per GPU: the native RCCL group (the group id broadcast from rank 0);
+    # W2V_BENCH_SHARE_GPU (ranks share cuda:0, RCCL needs one rank per GPU): one-rank native groups + gloo mean
+    rmode = args.replica_mode if args.replica_mode != "auto" else auto_replica_mode(world)
+    averager, rmode_used = make_averager(tr, mats, world, rank, rmode, not args.no_overlap, share)
     if args.sync_every > 0 or world == 1:
         rounds = n_rounds(n_sent * world, world, args.sync_every)
     else:  # every rank's shard has ~ the same words: the same round count everywhere
@@ -395,8 +391,8 @@ def main():
                 "vocab_size": V,
                 "global_batch": n_tok * world,
                 "parallelism": (f"dp{world}: full replica per GPU, corpus shard per GPU, RCCL all-reduce "
-                                f"of the updates, {rmode_used} (w2v_group, "
-                                f"{'overlapped' if not args.no_overlap else 'blocking'}) x{rounds} per step "
+                                f"of the updates, {rmode_used}, "
+                                f"{'overlapped' if not args.no_overlap else 'blocking'}, x{rounds} per step "
                                 f"(every {int(ids_h.size) // rounds} words of a shard)"
                                 if world > 1 else "dp1"),
                 "hot_rows": args.hot_rows,
@@ -418,7 +414,8 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    if isinstance(averager, NativeAverager):
+    if world > 1:
+        log(f"[bench] replica exchange: {rmode_used}, group {averager.info()}")
         averager.close()
     tr.close()
 

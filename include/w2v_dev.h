@@ -163,8 +163,10 @@ int w2v_dev_upload_corpus(w2v_dev* h, const int32_t* ids, int64_t n_tokens,
 /* Train on another handle's corpus (same device, same vocab) without a copy:
  * replicas sharing one GPU (Word2Vec::gpu_devices with a repeated device)
  * each train their own order slices of ONE resident corpus (configs[3]'s 10 B
- * tokens are 40 GB: eight copies would not fit one GPU). `src` must outlive
- * `h`'s training; h keeps its own order buffer and statistics copy. */
+ * tokens are 40 GB: eight copies would not fit one GPU). The corpus is
+ * reference-counted: destroying `src`, or uploading / adopting / sharing a new
+ * corpus into it, leaves h's copy resident until h lets go too. h keeps its
+ * own order buffer and statistics copy. */
 int w2v_dev_share_corpus(w2v_dev* h, w2v_dev* src);
 /* Replay mode: recorded draws in the reference's order (u per token; window
  * shrink per kept token; table positions per NS call) and their start offset

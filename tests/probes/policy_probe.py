@@ -7,9 +7,12 @@ usage: policy_probe.py <c3|c2|c1|c5> <variant> [<variant> ...]
   variant = name[:setter=value[,setter=value...]], setters: tau (hot-row
   threshold, rows), tau_nodes, hot (hot_rows), priv (private_rows), avg
   (private_average), flush (flush_centers), ctx (context_rows), ctxflush,
-  waves (max_waves); e.g. default tau1:tau=1 priv32:priv=32
+  waves (max_waves); e.g. default tau1:tau=1 priv32:priv=32; a key W2V_* is an
+  experiment knob set in the environment while the variant's handles are created
 Test infrastructure (reads the committed goldens; runs no oracle)."""
+import contextlib
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -21,8 +24,28 @@ ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT))
 
 
+def _kv(spec):
+    return dict(x.split("=") for x in spec.split(",") if x) if spec else {}
+
+
+@contextlib.contextmanager
+def knobs(spec):
+    """W2V_* keys of a variant in the environment (read at w2v_dev_create)."""
+    env = {k: v for k, v in _kv(spec).items() if k.startswith("W2V_")}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 def apply(t, spec):
-    kv = dict(x.split("=") for x in spec.split(",") if x) if spec else {}
+    kv = _kv(spec)
     if "tau" in kv or "tau_nodes" in kv:
         t.set_hot_auto(float(kv.get("tau", 0)), float(kv.get("tau_nodes", 1)))
     if "hot" in kv:
@@ -49,7 +72,9 @@ def headline(name, variants):
         got, ref, pol, t0 = [], [], None, time.time()
         for r in gold["scores"]:
             W0, C0, S0, key = G.init(name, r["seed"], counts.size)
-            t = gpu_trainer(counts, ids, soff, raw, w["mode"], w["dim"], w["negative"], w["alpha"], W0, C0, S0, key)
+            with knobs(spec):
+                t = gpu_trainer(counts, ids, soff, raw, w["mode"], w["dim"], w["negative"], w["alpha"], W0, C0, S0,
+                                key)
             apply(t, spec)
             st = t.train_epoch(0, G.order_of(r["seed"], soff.size - 1))
             pol = t.policy()
@@ -92,7 +117,8 @@ def c5(variants):
             cfg = Config(word_dim=t_["dim"], window=t_["window"], negative=t_["negative"], hs=False, cbow=False,
                          cbow_mean=True, iter=1, init_alpha=gold["alpha"], min_alpha=2.5e-6,
                          table_size=t_["table_size"])
-            d = device_from_oracle(o, cfg, initial=False)
+            with knobs(spec):
+                d = device_from_oracle(o, cfg, initial=False)
             d.set_update(N.W2V_UPDATE_SHARED_NEGATIVES)
             d.set_rng(N.W2V_RNG_PHILOX, 0x5EED0000 + r["seed"])
             d.set_schedule(N.W2V_SCHED_PARALLEL)

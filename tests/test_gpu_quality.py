@@ -10,10 +10,10 @@ seed-to-seed variance cancels and what is measured is the schedule:
     (north_star's "within +-1 point"), per corpus and mode (planted: mean of
     3 seeds; the text8-like corpus at 2 M tokens: one seed, since one wave
     trains ~60 K words/s);
-  * full concurrency with the default update policy: one-sided, the mean
-    delta must not fall below -1 (its damped, aggregated updates of the
-    frequent rows score above the sequential reference on these corpora,
-    DESIGN.md §2; a higher score is not a defect).
+  * full concurrency with the default update policy: the mean delta must
+    not fall below -1, nor rise past the measured delta + 2 (its damped,
+    aggregated updates of the frequent rows score above the sequential
+    reference on these corpora; FULL_HIGH).
 Unpaired gate (the reference's own mt19937 draws): the planted corpus in the
 4 modes against the REF-mode oracle goldens, one-sided. Deltas are printed
 (pytest -s) and recorded in DESIGN.md §2."""
@@ -98,10 +98,28 @@ def test_quality_paired_one_wave_within_1(name, mode):
     assert abs(d[0]) <= 1.0 and abs(d[1]) <= 1.0, (name, mode, got, ref)
 
 
+# Upper ends of the full-concurrency gates (no bound without an
+# upper end). The parallel policy scores above the sequential reference on
+# these corpora; high = the largest mean delta measured in the
+# round-3 / round-4 suites (profiles/r03c_gpu_tests.log, r04q_gpu_tests_final.log)
+# + 2 points (3 seeds; the per-seed spread is up to +-2.3) or + 3 (text8_small:
+# one seed). Measured means: planted SG-NS +10.74 / +5.16, SG-HS +3.51 / +0.72,
+# CBOW-NS +9.39 / +0.29, CBOW-HS +17.75 / +2.00; text8-like SG-NS +27.74 /
+# +1.97, CBOW-HS +22.18 / +13.61; text8_small SG-NS +18.98 / +6.57, CBOW-HS
+# +24.90 / +19.32.
+FULL_HIGH = {
+    ("planted", "sg_ns"): (12.8, 7.2), ("planted", "sg_hs"): (5.6, 2.8), ("planted", "cbow_ns"): (11.4, 2.3),
+    ("planted", "cbow_hs"): (19.8, 4.0), ("text8_like", "sg_ns"): (29.8, 4.0), ("text8_like", "cbow_hs"): (24.2, 15.7),
+    ("text8_small", "sg_ns"): (22.0, 9.6), ("text8_small", "cbow_hs"): (27.9, 22.4),
+}
+
+
 @pytest.mark.parametrize("name,mode", [(n, m) for n in paired.FULL_CORPORA for m in paired.PAIRED_MODES[n]])
-def test_quality_paired_full_concurrency_not_below(name, mode):
+def test_quality_paired_full_concurrency_bounded(name, mode):
     d, got, ref = _paired_delta(name, mode, max_waves=0)
+    hi = FULL_HIGH[(name, mode)]
     assert d[0] >= -1.0 and d[1] >= -1.0, (name, mode, got, ref)
+    assert d[0] <= hi[0] and d[1] <= hi[1], (name, mode, d, hi)
 
 
 @pytest.mark.parametrize("corpus", ["planted", "text8-like"])
@@ -137,16 +155,13 @@ def test_quality_shared_negatives_not_below_oracle(corpus):
 
 
 # configs[4]'s parallel schedule against the same formulation run
-# sequentially, paired: analogy -1.20 (per seed -2.23 / -1.13 / -0.22) and
-# -1.25 (-1.49 / -1.17 / -1.10) in two leases (r04a, r04b), similarity +2.8:
-# the concurrency of ~1000 centers each holding ~31 rows for a whole update
-# costs a point of analogy and gains three of similarity (the same kernel on
-# one workgroup matches the sequential run: 98.3 / 71.0 vs 98.3 / 69.7,
-# profiles/r03p_c5_quality_vs_waves.log; fewer waves or more / fewer atomic
-# rows all lose more analogy: profiles/r04b_policy_probe_c5.log,
-# r04c_policy_probe_c5.log). The analogy floor is the measured cost with a
-# quarter point of lease-to-lease spread, not north_star's point; DESIGN.md §2.
-C5_ANALOGY_LOW = -1.5
+# sequentially, paired, held to north_star's +-1 point both ways. Round 4 ran
+# 2 workgroups per CU on this V 98K corpus and cost -1.20 / -1.25 / -1.00
+# analogy (+2.8 similarity) in three leases; since round 5 the kernel caps its
+# workgroups in flight by vocab pressure (kSnPressure, w2v_dev.hip: 1 per CU
+# here) and measured +0.40 / +0.66 and +0.36 / +0.04 (profiles/r05a_*).
+# DESIGN.md §2.
+C5_BOUND = 1.0
 
 
 def test_quality_shared_negatives_c5_hyperparameters():
@@ -157,10 +172,8 @@ def test_quality_shared_negatives_c5_hyperparameters():
     build_vocab / init_weights(seed) / build_sample — on the same Philox key
     (0x5EED0000 + seed) and sentence order, so per seed the parallel schedule
     is the only difference and the corpus's seed-to-seed spread (the golden's
-    analogy spans 97.5-98.8) cancels. On the mean over the seeds: similarity
-    >= -1, analogy >= C5_ANALOGY_LOW (the measured cost of the parallel
-    schedule, below; round 3 compared unpaired 5-seed means against a
-    1.5-point bound set after a failure).
+    analogy spans 97.5-98.8) cancels. On the mean over the seeds: |delta| <=
+    1 point on analogy and on similarity (C5_BOUND, north_star).
     Also on analogy against the reference's per-pair SG-NS oracle at the same
     d / negative (quality_zipf_sg_ns_c5_oracle.json; the formulation scores
     +46 there)."""
@@ -205,7 +218,7 @@ def test_quality_shared_negatives_c5_hyperparameters():
     print(f"shared-negatives c5 d{t['dim']} neg{t['negative']} paired: gpu {got.mean(0).round(2)} oracle(sequential "
           f"minibatch) {ref.mean(0).round(2)} delta {dlt.mean(0).round(2)} per seed {dlt.round(2).tolist()}; "
           f"oracle(per-pair) {pp.round(2)} delta {(got.mean(0) - pp).round(2)}")
-    assert dlt.mean(0)[0] >= C5_ANALOGY_LOW and dlt.mean(0)[1] >= -1.0, (got, ref)
+    assert np.abs(dlt.mean(0)).max() <= C5_BOUND, (dlt.mean(0), got, ref)
     assert got.mean(0)[0] >= pp[0] - 1.0
 
 
@@ -218,17 +231,21 @@ def test_quality_shared_negatives_c5_hyperparameters():
 # the shipped throughput configuration (Philox, parallel schedule, the
 # library's automatic update policy for that vocabulary: hot-row threshold,
 # LDS-private rows, segments). Bounds on the mean paired delta over the
-# golden's seeds, (low, high) per metric: two-sided +-1 (north_star) where the
-# GPU lands within a point, one-sided (high = None) where the parallel update
-# policy scores ABOVE the sequential reference — measured (round 4, r04a /
-# r04b, 2 seeds): configs[2] analogy +1.2 to +2.1 (the damped,
-# aggregated updates of the frequent rows; similarity +0.03 at the shipped
-# hot-row threshold 1), configs[1] CBOW-HS +13.7 / +6.3, configs[0]
-# similarity +3.3. A higher score is not a defect; a lower one than -1 is.
+# golden's seeds, (low, high) per metric. Low is north_star's -1 point
+# everywhere. High is +1 (two-sided) where the GPU lands within a point of the
+# reference, else the measured delta + 1 (a bound with no upper
+# end passes a change that inflates scores by any amount): where the parallel
+# update policy scores ABOVE the sequential reference — measured (round 4,
+# r04a / r04b / r04n, 2 seeds): configs[2] analogy +1.80 to
+# +2.32 per seed (mean +1.97 / +2.06: the damped, aggregated updates of the
+# frequent rows), configs[1] CBOW-HS +13.66 / +6.34 (per seed +13.40..+13.91 /
+# +6.02..+6.67), configs[0] similarity +3.28 / +3.29 — the high bound is that
+# mean + 1. A policy change that moves a score past it fails here and is
+# explained in DESIGN.md §2 before the bound moves.
 HEADLINE_BOUNDS = {
-    "c3": {"analogy": (-1.0, None), "similarity": (-1.0, 1.0)},
-    "c2": {"analogy": (-1.0, None), "similarity": (-1.0, None)},
-    "c1": {"analogy": (-1.0, 1.0), "similarity": (-1.0, None)},
+    "c3": {"analogy": (-1.0, 3.1), "similarity": (-1.0, 1.0)},
+    "c2": {"analogy": (-1.0, 14.7), "similarity": (-1.0, 7.4)},
+    "c1": {"analogy": (-1.0, 1.0), "similarity": (-1.0, 4.3)},
 }
 
 
@@ -264,4 +281,4 @@ def test_quality_headline_scale(name):
           f"oracle {ref.mean(0).round(2)} delta {dl.round(2)} per seed {(got - ref).round(2).tolist()} policy {pol}")
     for k, metric in enumerate(("analogy", "similarity")):
         lo, hi = HEADLINE_BOUNDS[name][metric]
-        assert dl[k] >= lo and (hi is None or dl[k] <= hi), (name, metric, got, ref)
+        assert lo <= dl[k] <= hi, (name, metric, dl[k], (lo, hi), got, ref)

@@ -397,3 +397,30 @@ def test_shared_negatives_replicas_quality(R):
     d = np.array(many) - np.array(one)
     print(f"shared negatives, {R} replicas x{rounds}: one {np.round(one, 2)} many {np.round(many, 2)} delta {d.round(2)}")
     assert abs(d[0]) <= 1.0 and abs(d[1]) <= 1.0, (one, many)
+
+
+def test_shared_corpus_outlives_its_owner():
+    """w2v_dev_share_corpus is reference-counted: a borrower keeps
+    training on the shared ids after the owner is closed, and after the owner
+    uploads another corpus; it trains exactly what a handle with its own copy
+    trains (sequential Philox schedule: bit-identical)."""
+    o, (own, ref) = _pair_of_handles("sg_ns")
+    cfg = ref.cfg
+    borrower = device_from_oracle(o, cfg, initial=False)
+    borrower.share_corpus(own)
+    ids, soff = o.samples()
+    own.upload_corpus(ids[: soff[3]], soff[:4], int(soff[3]))  # the owner moves on to another corpus ...
+    own.close()  # ... and is gone
+    order = np.random.default_rng(4).permutation(soff.size - 1)
+    out = []
+    for d in (borrower, ref):
+        d.set_rng(N.W2V_RNG_PHILOX, 77)
+        d.set_schedule(N.W2V_SCHED_SEQUENTIAL)
+        d.set_progress(0)
+        st = d.train_epoch(0, order)
+        assert st["words"] == ids.size
+        out.append(d.download_model())
+        d.close()
+    for a, b in zip(*out):
+        if a is not None:
+            np.testing.assert_array_equal(a, b)

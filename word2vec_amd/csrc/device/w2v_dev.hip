@@ -80,7 +80,8 @@ struct Knobs {
   int64_t sn_atomic_rows = -1;   // W2V_SN_ATOMIC_ROWS
   int scale_resident = 0;        // W2V_SCALE_RESIDENT=1: flush scales from the chip's resident workgroups, not the launch's grid
   double priv_tail_avg = -1;     // W2V_PRIV_TAIL_AVG: private_average of the NS output rows past the 64th (0 = plain sum)
-  std::string desc;              // "NAME=value ..." of the variables that were set
+  int sn_per_cu = 0;             // W2V_SN_PER_CU: shared-negatives workgroups per CU (cap)
+  std::string desc;             // "NAME=value ..." of the variables that were set
 };
 
 static Knobs read_knobs() {
@@ -99,8 +100,20 @@ static Knobs read_knobs() {
   if (const char* v = get("W2V_SN_ATOMIC_ROWS")) k.sn_atomic_rows = std::max<int64_t>(0, std::atoll(v));
   if (const char* v = get("W2V_SCALE_RESIDENT")) k.scale_resident = std::atoi(v) != 0;
   if (const char* v = get("W2V_PRIV_TAIL_AVG")) k.priv_tail_avg = std::max(0.0, std::atof(v));
+  if (const char* v = get("W2V_SN_PER_CU")) k.sn_per_cu = std::max(0, std::atoi(v));
   return k;
 }
+
+// A resident corpus (token ids + sentence offsets). Handles on one device may
+// train on one copy (w2v_dev_share_corpus: replicas of configs[3]'s 40 GB of
+// ids); each holds a reference and the last one to let go frees it, so an
+// owner that is destroyed or re-uploads its corpus never frees buffers a
+// borrower's kernels still read.
+struct CorpusBuf {
+  int32_t* ids = nullptr;
+  int64_t* soff = nullptr;
+  int refs = 1;
+};
 
 struct w2v_dev {
   w2v_dev_config cfg{};
@@ -131,7 +144,7 @@ struct w2v_dev {
   int64_t n_codes = 0;
   int32_t* ids = nullptr;
   int64_t* soff = nullptr;
-  bool corpus_borrowed = false;    // ids / soff belong to another handle on this device (w2v_dev_share_corpus)
+  CorpusBuf* corpus = nullptr;     // owns ids / soff, shared with the handles training on it
   int64_t n_tok = 0, n_sent = 0, train_words = 0;
   int64_t max_len = 0;        // longest sentence (tokens)
   int64_t* order = nullptr;
@@ -320,16 +333,17 @@ int set_device(w2v_dev* h) {
   return W2V_OK;
 }
 
-// Drop the handle's corpus: its own buffers are freed, a borrowed one
-// (w2v_dev_share_corpus) is only released (its owner frees it).
+// Drop the handle's reference to its corpus; the buffers are freed with the
+// last reference (w2v_dev_share_corpus).
 void release_corpus(w2v_dev* h) {
-  if (!h->corpus_borrowed) {
-    dfree(h->ids);
-    dfree(h->soff);
+  if (h->corpus && --h->corpus->refs == 0) {
+    dfree(h->corpus->ids);
+    dfree(h->corpus->soff);
+    delete h->corpus;
   }
+  h->corpus = nullptr;
   h->ids = nullptr;
   h->soff = nullptr;
-  h->corpus_borrowed = false;
   dfree(h->order);
   h->corpus_ready = false;
 }
@@ -414,8 +428,7 @@ void w2v_dev_destroy(w2v_dev* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (!h->model_bound) { dfree(h->W); dfree(h->C); dfree(h->S); }
   dfree(h->keep); dfree(h->table); dfree(h->codes); dfree(h->points); dfree(h->coff);
-  if (!h->corpus_borrowed) { dfree(h->ids); dfree(h->soff); }
-  dfree(h->order); dfree(h->replay); dfree(h->replay_off);
+  release_corpus(h); dfree(h->replay); dfree(h->replay_off);
   dfree(h->counters); dfree(h->work);
   dfree(h->scratch_f); dfree(h->scratch_codes); dfree(h->xfer_f); dfree(h->wide_scratch);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
@@ -745,9 +758,12 @@ int w2v_dev_upload_corpus(w2v_dev* h, const int32_t* ids, int64_t n_tok, const i
   if (train_words <= 0 && n_tok > 0) return fail(W2V_ERR_ARG, "train_words must be > 0");
   if (set_device(h)) return W2V_ERR_HIP;
   release_corpus(h);
-  HIP_TRY(hipMalloc(&h->ids, (n_tok > 0 ? n_tok : 1) * sizeof(int32_t)));
+  h->corpus = new CorpusBuf();
+  HIP_TRY(hipMalloc(&h->corpus->ids, (n_tok > 0 ? n_tok : 1) * sizeof(int32_t)));
+  HIP_TRY(hipMalloc(&h->corpus->soff, (n_sent + 1) * sizeof(int64_t)));
+  h->ids = h->corpus->ids;
+  h->soff = h->corpus->soff;
   if (n_tok > 0) HIP_TRY(hipMemcpy(h->ids, ids, n_tok * sizeof(int32_t), hipMemcpyHostToDevice));
-  HIP_TRY(hipMalloc(&h->soff, (n_sent + 1) * sizeof(int64_t)));
   HIP_TRY(hipMemcpy(h->soff, soff, (n_sent + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
   HIP_TRY(hipMalloc(&h->order, (n_sent > 0 ? n_sent : 1) * sizeof(int64_t)));
   h->n_tok = n_tok;
@@ -783,9 +799,12 @@ int w2v_dev_adopt_corpus(w2v_dev* h, w2v_ingest* g) {
   std::vector<int64_t> hist((size_t)h->V, 0);
   for (int64_t w = 0; w < v.n_vocab; ++w) hist[(size_t)w] = v.hist[w];
   release_corpus(h);
-  HIP_TRY(hipMalloc(&h->ids, (v.n_ids > 0 ? v.n_ids : 1) * sizeof(int32_t)));
+  h->corpus = new CorpusBuf();
+  HIP_TRY(hipMalloc(&h->corpus->ids, (v.n_ids > 0 ? v.n_ids : 1) * sizeof(int32_t)));
+  HIP_TRY(hipMalloc(&h->corpus->soff, (v.n_sentences + 1) * sizeof(int64_t)));
+  h->ids = h->corpus->ids;
+  h->soff = h->corpus->soff;
   if (v.n_ids > 0) HIP_TRY(hipMemcpy(h->ids, v.ids, v.n_ids * sizeof(int32_t), hipMemcpyDeviceToDevice));
-  HIP_TRY(hipMalloc(&h->soff, (v.n_sentences + 1) * sizeof(int64_t)));
   HIP_TRY(hipMemcpy(h->soff, v.offsets, (v.n_sentences + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice));
   HIP_TRY(hipMalloc(&h->order, (v.n_sentences > 0 ? v.n_sentences : 1) * sizeof(int64_t)));
   h->n_tok = v.n_ids;
@@ -807,11 +826,13 @@ int w2v_dev_share_corpus(w2v_dev* h, w2v_dev* src) {
   if (h->V != src->V) return fail(W2V_ERR_ARG, "w2v_dev_share_corpus: the vocabularies differ");
   if (set_device(h)) return W2V_ERR_HIP;
   HIP_TRY(hipStreamSynchronize(h->stream));
+  if (h->corpus == src->corpus) return W2V_OK;
   release_corpus(h);
   HIP_TRY(hipMalloc(&h->order, (src->n_sent > 0 ? src->n_sent : 1) * sizeof(int64_t)));
+  h->corpus = src->corpus;
+  ++h->corpus->refs;
   h->ids = src->ids;
   h->soff = src->soff;
-  h->corpus_borrowed = true;
   h->n_tok = src->n_tok;
   h->n_sent = src->n_sent;
   h->n_order = 0;
@@ -1051,6 +1072,9 @@ static std::pair<int64_t, int64_t> auto_hot(w2v_dev* h, double waves, bool share
   return {std::min<int64_t>(V, std::max<int64_t>(rows, 64)), nodes};
 }
 
+// Shared-negatives workgroups in flight per (vocab row / row held by a center); launch_train.
+constexpr double kSnPressure = 0.06;
+
 // The shared-negatives minibatch covers skip-gram NS only: a 16 x 16 MFMA tile
 // holds <= 16 unique context rows (2 * window <= 16) and the center + <= 15
 // negatives; its draws are Philox (the reference has no such path to replay).
@@ -1279,11 +1303,24 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
       int per_cu = 0;
       HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sn_fn, threads, 0));
       if (per_cu < 1) per_cu = 1;
-      // Concurrency a vocab can take (measured on the planted corpora: quality
-      // holds at 1 workgroup per CU for V = 3.4K and 2 for V = 98K, and
-      // collapses at 4): every center holds ~22 rows for its whole update, so
-      // a small vocab's frequent rows are held by hundreds of workgroups at once.
-      if (h->max_waves == 0) per_cu = std::min(per_cu, h->V < 16384 ? 1 : h->V < 524288 ? 2 : per_cu);
+      // Concurrency a vocab can take: every center holds its 2 window + negative
+      // + 1 rows for its whole update, so a small vocab's frequent rows are held
+      // by hundreds of workgroups at once. Workgroups in flight are capped at
+      // kSnPressure x V / (rows per center) (at least one per CU). Measured on
+      // the text8-like gate corpus (V 98K, d512, negative 15, window 5: 26 rows;
+      // the paired gate against the sequential minibatch, 3 seeds, two runs
+      // each, profiles/r05a_2_policy_probe.log): 2 workgroups per CU -1.06 /
+      // +2.57 and -0.78 / +3.00 (analogy / similarity), 1 per CU +0.40 / +0.66
+      // and +0.36 / +0.04. The cap allows 0.06 x 98K / 26 = 226 workgroups there
+      // (-> 1 per CU) and leaves configs[4]'s V 740K at full occupancy (4 per CU:
+      // 1708). Round 1 measured quality holding at 1 per CU for V 3.4K and
+      // collapsing at 4 for V 98K (profiles/r01_sn_residency_experiment.log).
+      if (h->max_waves == 0) {
+        const double rows = 2.0 * h->cfg.window + h->cfg.negative + 1.0;
+        const double cap = kSnPressure * (double)h->V / rows / (double)std::max(1, h->n_cu);
+        per_cu = std::max(1, std::min(per_cu, (int)cap));
+      }
+      if (h->knobs.sn_per_cu > 0) per_cu = std::min(per_cu, h->knobs.sn_per_cu);  // experiments
       g_res = (int64_t)per_cu * h->n_cu;
       g = std::min<int64_t>(g_res, count);
       if (h->max_waves > 0) g = std::max<int64_t>(1, std::min<int64_t>(g, h->max_waves / sn_waves));

@@ -50,7 +50,8 @@ constexpr int kWave = 64;
 // bit 1 skips the hot-row atomics of the targets, bit 2 the global atomics of
 // the private-row flushes, bit 4 the hot context-row atomics of CBOW; in the
 // shared-negatives kernel bit 8 skips the staged atomic rows, bit 16 the
-// private-row flush atomics, bit 32 makes the coherent (sc1) stores plain.
+// private-row flush atomics, bit 32 makes the coherent (sc1) stores plain;
+// bit 64 skips the per-pair kernels' plain (Hogwild) row stores.
 #ifndef W2V_EXP_SKIP
 #define W2V_EXP_SKIP 0
 #endif
@@ -369,7 +370,7 @@ __device__ __forceinline__ void add_to_row(float* M, int64_t row, bool hot, int6
     load_row<NV>(M, row, pitch, d, lane, false, cur);
 #pragma unroll
     for (int v = 0; v < NV; ++v) cur[v] += delta[v];
-    store_row<NV>(M, row, pitch, d, lane, cur);
+    if (!(W2V_EXP_SKIP & 64)) store_row<NV>(M, row, pitch, d, lane, cur);
   }
 }
 
@@ -611,7 +612,7 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
       } else {
 #pragma unroll
         for (int v = 0; v < NV; ++v) r[t][v] += delta[v];
-        store_row<NV>(M, rows[t], pitch, d, lane, r[t]);
+        if (!(W2V_EXP_SKIP & 64)) store_row<NV>(M, rows[t], pitch, d, lane, r[t]);
       }
     }
   }
@@ -751,7 +752,7 @@ __device__ __forceinline__ void hs_apply(const TrainArgs& a, int T, int row_l, i
       } else {
 #pragma unroll
         for (int v = 0; v < NV; ++v) r[t][v] += delta[v];
-        store_row<NV>(a.S, row, a.pitch, a.dim, lane, r[t]);
+        if (!(W2V_EXP_SKIP & 64)) store_row<NV>(a.S, row, a.pitch, a.dim, lane, r[t]);
       }
     }
   }
@@ -1168,7 +1169,7 @@ __device__ __forceinline__ void cbow_tail(const TrainArgs& a, float* lds, int i,
         } else {
 #pragma unroll
           for (int v = 0; v < NV; ++v) cur[t][v] += g[v];
-          store_row<NV>(a.C, row, a.pitch, a.dim, lane, cur[t]);
+          if (!(W2V_EXP_SKIP & 64)) store_row<NV>(a.C, row, a.pitch, a.dim, lane, cur[t]);
         }
       }
   }

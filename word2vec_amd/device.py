@@ -138,7 +138,8 @@ class DeviceTrainer:
         self.n_sent = o.size - 1
 
     def share_corpus(self, src: "DeviceTrainer"):
-        """Train on src's resident corpus (same device and vocab; no copy; src must outlive this handle)."""
+        """Train on src's resident corpus (same device and vocab; no copy). The C side counts references,
+        so src may be closed first; the corpus is freed with the last handle holding it."""
         self._chk(self.lib.w2v_dev_share_corpus(self.h, src.h), "w2v_dev_share_corpus")
         self.n_sent = src.n_sent
 

@@ -22,7 +22,10 @@ the frequent rows, plain averaging of short shards loses the rare rows'
 progress; measured tables in DESIGN.md §6), with the exchange overlapped.
 `TorchAverager` (model averaging
 over torch.distributed) is what the CPU tests run on the gloo backend to
-exercise the round logic, which is the same object code.
+exercise the round logic, which is the same object code. `make_averager` is
+bench.py's per-rank construction (the group id broadcast included); the CPU
+tests drive it against a stub of the C-ABI's group calls, and on a one-GPU box
+it builds the `RehearsalAverager`.
 
 The alpha schedule stays global without a collective per round: each rank
 knows every rank's words per round (exchanged once, `global_round_words`), sets
@@ -194,6 +197,54 @@ def group_unique_id() -> bytes:
     buf = (C.c_uint8 * N.W2V_GROUP_ID_BYTES)()
     N.check(lib, lib.w2v_group_unique_id(buf), "w2v_group_unique_id")
     return bytes(buf)
+
+
+class RehearsalAverager:
+    """The N > 1 path rehearsed with every rank on ONE GPU (RCCL refuses two
+    ranks on one device: "Duplicate GPU detected"). Each rank runs the native
+    exchange on a one-rank RCCL communicator — the same group calls per round
+    (delta kernel, ncclAllReduce on the communication stream, fold; with one
+    rank an identity on the model) — and the cross-process combination is the
+    mean over torch.distributed (gloo). Only ncclCommInitRank with more than
+    one rank, and the multi-rank all-reduce, are new on a multi-GPU node."""
+
+    def __init__(self, native: NativeAverager, torch_avg: TorchAverager):
+        self.native, self.torch_avg = native, torch_avg
+
+    def average(self) -> None:
+        self.native.average()
+        self.torch_avg.average()
+
+    def finish(self) -> None:
+        self.native.finish()
+
+    def info(self) -> dict:
+        return self.native.info()
+
+    def close(self) -> None:
+        self.native.close()
+
+
+def make_averager(trainer, mats, world: int, rank: int, mode: str, overlap: bool, share_gpu: bool = False):
+    """The replica exchange of bench.py --gpus N, one call per rank (world > 1
+    needs torch.distributed initialised: the group id travels over it):
+      * world 1: a no-op;
+      * one rank per GPU: the native RCCL group over all ranks (rank 0 makes
+        the unique id, broadcast to the others) in `mode`;
+      * share_gpu (the one-GPU rehearsal): RehearsalAverager — rank 0 makes one
+        id per rank, broadcast the same way, each rank a one-rank native group,
+        the mean over torch.distributed across the processes.
+    Returns (averager, description)."""
+    if world == 1:
+        return TorchAverager(mats, 1), "dp1"
+    if not share_gpu:
+        uid = [group_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        return NativeAverager([trainer], uid[0], world, rank, overlap=overlap, mode=mode), f"{mode} (w2v_group)"
+    uids = [[group_unique_id() for _ in range(world)] if rank == 0 else None]
+    dist.broadcast_object_list(uids, src=0)
+    native = NativeAverager([trainer], uids[0][rank], 1, 0, overlap=overlap, mode=mode)
+    return RehearsalAverager(native, TorchAverager(mats, world)), "rehearsal: one-rank w2v_group per process + gloo mean"
 
 
 def train_rounds(trainer, averager, order_dev: torch.Tensor, epoch: int, rounds: int, progress_base: int,
