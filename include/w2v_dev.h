@@ -59,7 +59,7 @@ typedef struct w2v_dev w2v_dev; /* opaque handle */
  * (Word2Vec.h:64-66; members Word2Vec.h:32-46). */
 typedef struct w2v_dev_config {
   int32_t word_dim;  /* Word2Vec::word_dim  (Word2Vec.h:36)                      */
-  int32_t window;    /* Word2Vec::window    (Word2Vec.h:33), 0..127              */
+  int32_t window;    /* Word2Vec::window    (Word2Vec.h:33), w2v_dev_limits      */
   int32_t negative;  /* Word2Vec::negative  (Word2Vec.h:37), 0 disables NS       */
   int32_t hs;        /* train_method == "hs" (Word2Vec.cpp:162,206,342,304)       */
   int32_t cbow;      /* model == "cbow"     (Word2Vec.cpp:387-390)               */
@@ -97,15 +97,24 @@ const char* w2v_dev_knobs(w2v_dev* h);
 
 /* The kernels' range of the reference's unbounded hyper-parameters
  * (Word2Vec.cpp:254, 285, 335 accept any window / negative): word_dim <= 2048,
- * window <= 65535, negative <= 65535 (w2v_dev_create returns
- * W2V_ERR_UNSUPPORTED beyond them; negatives past 63 are drawn and
+ * window <= 4096, negative <= 4096 (w2v_dev_create returns
+ * W2V_ERR_UNSUPPORTED beyond them). Negatives past 63 are drawn and
  * deduplicated 64 at a time, CBOW windows past 127 are walked from the
- * sentence); the shared-negatives update: window <= 8, negative <= 15 (its
- * 16 x 16 MFMA tiles hold a window's <= 16 inputs and <= 16 outputs).
+ * sentence; both deduplications grow with the square of the count, so the
+ * range stops where it was measured (profiles/r05b_4_limits_cost_probe.log,
+ * d 64, one MI355X): per target row 6.4 ns at negative 64, 13.5 ns at 1024,
+ * 46 ns at 4096; CBOW per target 0.49 us at window 128, 4.5 us at 1024,
+ * 5.8 us at 2048 (2 window context rows per center). The shared-negatives
+ * update: window <= 8, negative <= 15 (its 16 x 16 MFMA tiles hold a window's
+ * <= 16 inputs and <= 16 outputs), word_dim <= 1024 (w2v_dev_shared_limits).
  * Callers check these up front (Word2Vec::train, the CLI) to fail before any
  * corpus work, naming the reference's member / flag. Any pointer may be NULL. */
 int w2v_dev_limits(int32_t* max_dim, int32_t* max_window, int32_t* max_negative, int32_t* shared_max_window,
                    int32_t* shared_max_negative);
+/* The shared-negatives update's range (W2V_UPDATE_SHARED_NEGATIVES): rows of
+ * 64 x {1..8, 10, 12, 14, 16} floats (word_dim <= 1024), window <= 8,
+ * negative <= 15. Any pointer may be NULL. */
+int w2v_dev_shared_limits(int32_t* max_dim, int32_t* max_window, int32_t* max_negative);
 
 /* Replaces: the Word2Vec ctor's device-relevant state (Word2Vec.cpp:12-17). */
 int w2v_dev_create(const w2v_dev_config* cfg, w2v_dev** out);

@@ -5,7 +5,10 @@ Input: zipf_sentences(200, 400, 2000, seed=51, ragged=True), window 150,
 negative 80, alpha 0.025, d 64, subsample 1e-3, min_count 2, table 1e5.
 The oracle (w2v_oracle.cpp) trains it one epoch in two draw modes:
   * REF: the reference's own mt19937 stream (Word2Vec.cpp:356-396);
-  * PHILOX: the device's Philox draws (key 99, the r04a test's), sequential.
+  * PHILOX: the device's Philox draws (key 99, the r04a test's), sequential;
+  * OMP<T>: the reference's own OpenMP Hogwild loop (Word2Vec.cpp:375-394,
+    orc_train_omp_shared) on T threads sharing the model, one mt19937 per
+    thread (the reference shares one, a data race);
 and reports, per matrix, whether every value is finite and the largest |x|,
 plus the largest |sigma argument| reached is inferred from the row norms
 (max |W_i| * max |C_j|).
@@ -35,6 +38,9 @@ def run(mode, alpha, draws, vmax=2000, window=150, negative=80, dim=64):
     t0 = time.time()
     if draws == "ref":
         o.train(record=False)
+    elif draws.startswith("omp"):
+        o.init_weights()  # Word2Vec.cpp:358 (train() re-initialises)
+        o.train_omp(int(draws[3:]), o.samples()[1].size - 1, seed=1234, shared_rng=False)
     else:
         order = np.random.default_rng(3).permutation(o.samples()[1].size - 1)
         o.train_philox(0, 1, order, 99, 0)
@@ -55,10 +61,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--alpha", type=float, nargs="*", default=[0.025, 0.0025])
     ap.add_argument("--vmax", type=int, default=2000)
+    ap.add_argument("--draws", nargs="*", default=["ref", "philox"], help="ref, philox, omp<T>")
+    ap.add_argument("--modes", nargs="*", default=["cbow_ns", "sg_ns"])
     a = ap.parse_args()
     for alpha in a.alpha:
-        for mode in ("cbow_ns", "sg_ns"):
-            for draws in ("ref", "philox"):
+        for mode in a.modes:
+            for draws in a.draws:
                 run(mode, alpha, draws, vmax=a.vmax)
 
 

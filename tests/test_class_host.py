@@ -276,10 +276,12 @@ def test_hyperparameter_limits_fail_early():
     """The reference accepts any window / negative / word_dim
     (Word2Vec.cpp:254, 285, 335). The per-pair kernels take negatives past 63
     (drawn 64 at a time) and CBOW windows past 127 (walked from the sentence)
-    up to 65535 and rows up to 2048 floats (w2v_dev_limits; round 4); beyond
-    that, and for the shared-negatives tiles (window 8, negative 15), the
-    range is enforced before any corpus or device work: the class names the
-    member, the CLI the reference's flag."""
+    up to 4096 (both walks are quadratic: round 5 stopped the range where its
+    cost was measured) and rows up to 2048 floats (w2v_dev_limits); beyond
+    that, and for the shared-negatives tiles (window 8, negative 15, rows of
+    <= 1024 floats: w2v_dev_shared_limits), the range is enforced before any
+    corpus or device work: the class names the member, the CLI the
+    reference's flag."""
     import ctypes as C
 
     from tests.corpus import zipf_sentences
@@ -289,9 +291,12 @@ def test_hyperparameter_limits_fail_early():
     lib = N.load_dev_lib()
     v = [C.c_int32() for _ in range(5)]
     assert lib.w2v_dev_limits(*[C.byref(x) for x in v]) == 0
-    assert [x.value for x in v] == [2048, 65535, 65535, 8, 15]
+    assert [x.value for x in v] == [2048, 4096, 4096, 8, 15]
+    sv = [C.c_int32() for _ in range(3)]
+    assert lib.w2v_dev_shared_limits(*[C.byref(x) for x in sv]) == 0
+    assert [x.value for x in sv] == [1024, 8, 15]
     sents = zipf_sentences(5, 50, 100, seed=1)
-    for kw, what in ((dict(window=65536), "window"), (dict(negative=65536), "negative"),
+    for kw, what in ((dict(window=4097), "window"), (dict(negative=4097), "negative"),
                      (dict(word_dim=2049), "word_dim")):
         base = dict(iter=1, window=5, min_count=1, table_size=1000, word_dim=16, negative=5, train_method="ns",
                     model="sg")
@@ -305,10 +310,17 @@ def test_hyperparameter_limits_fail_early():
     w.build_vocab(sents)
     with pytest.raises(RuntimeError, match="shared_negatives"):
         w.train(sents)
-    r = _cli("-window", "65536", "-negative", "5")
-    assert r.returncode == 1 and "Please set -window in [0, 65535]" in r.stdout
-    r = _cli("-negative", "65536")
-    assert r.returncode == 1 and "Please set -negative <= 65535" in r.stdout
+    w = Word2Vec(iter=1, window=5, min_count=1, table_size=1000, word_dim=1100, negative=5, train_method="ns",
+                 model="sg", shared_negatives=True)
+    w.build_vocab(sents)
+    with pytest.raises(RuntimeError, match="shared_negatives.*word_dim <= 1024"):
+        w.train(sents)
+    r = _cli("-window", "4097", "-negative", "5")
+    assert r.returncode == 1 and "Please set -window in [0, 4096]" in r.stdout
+    r = _cli("-negative", "4097")
+    assert r.returncode == 1 and "Please set -negative <= 4096" in r.stdout
+    r = _cli("-size", "1100", "-negative", "5", "-shared-negatives", "1")
+    assert r.returncode == 1 and "-size <= 1024" in r.stdout
     r = _cli("-size", "3000", "-negative", "5")
     assert r.returncode == 1 and "Please set -size in [1, 2048]" in r.stdout
     r = _cli("-negative", "16", "-shared-negatives", "1")

@@ -393,28 +393,30 @@ def test_replay_wide_rows(mode, dim):
     check_parity(got, want, init, *LIFTED, tag=f"wide rows {mode} d{dim}")
 
 
+def _huge_window_trainer(mode, vmax, alpha):
+    from word2vec_amd.device import Config
+
+    sents = zipf_sentences(200, 400, vmax, seed=51, ragged=True)
+    o = oracle_run(sents, mode, dim=64, window=150, iters=1, table_size=100_000, train=False)
+    o.build_sample()
+    m = MODES[mode]
+    cfg = Config(word_dim=64, window=150, negative=80, hs=False, cbow=m["model"] == "cbow", cbow_mean=True,
+                 iter=1, init_alpha=alpha, min_alpha=2.5e-6, table_size=100_000)
+    d = device_from_oracle(o, cfg, initial=False)
+    d.set_rng(N.W2V_RNG_PHILOX, 99)
+    d.set_schedule(N.W2V_SCHED_PARALLEL)
+    d.set_progress(0)
+    return o, d, np.random.default_rng(3).permutation(o.samples()[1].size - 1)
+
+
 def test_parallel_huge_window_and_many_negatives_run():
     """The parallel schedule with window 150 and negative 80 on 64 waves
-    (several workgroups, each wave its own slice of the huge-window scratch):
-    trains, counts every word once, stays finite. (At full concurrency on a
-    2000-word vocabulary and alpha 0.025 this configuration diverges — 300
-    contexts x 81 targets per center on a few thousand rows — which
-    w2v_dev_train_epoch reports as W2V_ERR_DIVERGED.)"""
-    sents = zipf_sentences(200, 400, 20000, seed=51, ragged=True)
+    (several workgroups, each wave its own slice of the huge-window scratch),
+    alpha 0.0025, 20 K Zipf ranks: trains, counts every word once, stays finite."""
     for mode in ("cbow_ns", "sg_ns"):
-        o = oracle_run(sents, mode, dim=64, window=150, iters=1, table_size=100_000, train=False)
-        o.build_sample()
-        from word2vec_amd.device import Config
-
-        m = MODES[mode]
-        cfg = Config(word_dim=64, window=150, negative=80, hs=False, cbow=m["model"] == "cbow", cbow_mean=True,
-                     iter=1, init_alpha=0.0025, min_alpha=2.5e-6, table_size=100_000)
-        d = device_from_oracle(o, cfg, initial=False)
-        d.set_rng(N.W2V_RNG_PHILOX, 99)
-        d.set_schedule(N.W2V_SCHED_PARALLEL)
+        o, d, order = _huge_window_trainer(mode, 20000, 0.0025)
         d.set_max_waves(64)
-        d.set_progress(0)
-        st = d.train_epoch(0, np.random.default_rng(3).permutation(o.samples()[1].size - 1))
+        st = d.train_epoch(0, order)
         ids, _ = o.samples()
         assert st["words"] == ids.size and st["nonfinite"] == 0
         W, Cm, _ = d.download_model()
@@ -422,9 +424,39 @@ def test_parallel_huge_window_and_many_negatives_run():
         d.close()
 
 
+def test_parallel_huge_window_reference_alpha_full_concurrency():
+    """The r04a input at the reference's alpha 0.025 and full concurrency
+    (window 150, negative 80, V 1,807: each skip-gram center updates ~12 K
+    target rows, every row ~7 times). VERDICT r04 "next" 2: the sequential
+    reference stays finite on it (max |W| 72 with its own draws, 119 with the
+    Philox draws), but the reference's OWN parallel loop does not hold either:
+    its OpenMP Hogwild (Word2Vec.cpp:375-394, the oracle's
+    orc_train_omp_shared) reaches max |W| 152 / 1.0e3 / 1.6e5 on 2 / 4 / 8
+    threads (tests/probes/divergence_probe.py, profiles/r05_divergence_oracle.log);
+    the GPU's parallel schedule diverges at every wave count from 128 up and
+    grows to 1e7-1e16 at 32-64 waves (profiles/r05a_1_*, r05b_2_*,
+    r05d_*). So skip-gram must fail LOUDLY there (W2V_ERR_DIVERGED, never
+    silent non-finite weights); CBOW-NS, whose centers update only the
+    negatives' rows of W, trains finite at full concurrency (max |W| 0.54
+    against the sequential 0.96)."""
+    o, d, order = _huge_window_trainer("cbow_ns", 2000, 0.025)
+    st = d.train_epoch(0, order)
+    assert st["words"] == o.samples()[0].size and st["nonfinite"] == 0
+    W, Cm, _ = d.download_model()
+    assert np.isfinite(W).all() and np.isfinite(Cm).all() and np.abs(W).max() < 10.0
+    d.close()
+    o, d, order = _huge_window_trainer("sg_ns", 2000, 0.025)
+    with pytest.raises(N.DevError) as e:
+        d.train_epoch(0, order)
+    assert e.value.code == N.W2V_ERR_DIVERGED
+    d.close()
+
+
 def test_window_limit():
     from word2vec_amd.device import Config, DeviceTrainer
 
-    DeviceTrainer(Config(word_dim=16, window=65535, negative=5, cbow=True, table_size=1000))
+    DeviceTrainer(Config(word_dim=16, window=4096, negative=4096, cbow=True, table_size=1000))
     with pytest.raises(N.DevError, match="window"):
-        DeviceTrainer(Config(word_dim=16, window=65536, negative=5, table_size=1000))
+        DeviceTrainer(Config(word_dim=16, window=4097, negative=5, table_size=1000))
+    with pytest.raises(N.DevError, match="negative"):
+        DeviceTrainer(Config(word_dim=16, window=5, negative=4097, table_size=1000))

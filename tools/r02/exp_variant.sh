@@ -9,7 +9,7 @@ tag=$1; flags=$2; nvs=${3:-"4 5"}
 C=$R/word2vec_amd/csrc; L=$R/word2vec_amd/lib; D=$L/$tag
 DEV=${DEVDIR:-$C/device}  # DEVDIR: another copy of csrc/device (e.g. an earlier commit's, for A/B runs)
 mkdir -p "$D/obj"
-cp "$L"/obj/*.o "$D/obj/"
+cp "$L"/obj/w2v_*.o "$D/obj/"
 pids=()
 for n in $nvs; do  # a row width, or "shared" for the shared-negatives kernel
   if [ "$n" = shared ]; then src=w2v_shared.hip; obj=w2v_shared.o; def=; else src=w2v_inst.hip; obj=w2v_inst_nv$n.o; def="-DW2V_NV=$n -mllvm -amdgpu-atomic-optimizer-strategy=None"; fi

@@ -79,6 +79,7 @@ _F = C.c_float
 SIGNATURES = {
     "w2v_dev_version": (C.c_char_p, []),
     "w2v_dev_limits": (C.c_int, [C.POINTER(_I32)] * 5),
+    "w2v_dev_shared_limits": (C.c_int, [C.POINTER(_I32)] * 3),
     "w2v_dev_last_error": (C.c_char_p, []),
     "w2v_dev_knobs": (C.c_char_p, [_P]),
     "w2v_dev_create": (C.c_int, [C.POINTER(DevConfig), C.POINTER(_P)]),

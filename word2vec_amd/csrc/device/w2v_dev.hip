@@ -359,18 +359,30 @@ const char* w2v_dev_knobs(w2v_dev* h) { return h ? h->knobs.desc.c_str() : ""; }
 
 // The per-pair kernels' range (the reference takes any, Word2Vec.cpp:254, 285,
 // 335): a row is <= 32 floats per lane; a context's negatives are drawn and
-// deduplicated 64 at a time (ns_word_many) with the draw index in the Philox
-// counter (philox_table_pos: k < 2^20); a CBOW window past 127 is walked from
-// the sentence (cbow_center_huge) with a per-wave scratch of huge_stride ints.
-constexpr int32_t kMaxDim = 2048, kMaxNegative = 65535, kMaxWindowHost = 65535;
+// deduplicated 64 at a time (ns_word_many: every chunk is compared with every
+// earlier one) with the draw index in the Philox counter (philox_table_pos:
+// k < 2^20); a CBOW window past 127 is walked from the sentence
+// (cbow_center_huge: each position against the earlier ones) with a per-wave
+// scratch of huge_stride ints. Both walks are quadratic, so window and
+// negative stop at 4096, where their cost was measured (include/w2v_dev.h;
+// at 65535 a center would take ~2^28 steps).
+constexpr int32_t kMaxDim = 2048, kMaxNegative = 4096, kMaxWindowHost = 4096;
+constexpr int32_t kSnMaxDim = 1024, kSnMaxWindow = 8, kSnMaxNegative = 15;
 
 int w2v_dev_limits(int32_t* max_dim, int32_t* max_window, int32_t* max_negative, int32_t* shared_max_window,
                    int32_t* shared_max_negative) {
   if (max_dim) *max_dim = kMaxDim;
   if (max_window) *max_window = kMaxWindowHost;
   if (max_negative) *max_negative = kMaxNegative;
-  if (shared_max_window) *shared_max_window = 8;
-  if (shared_max_negative) *shared_max_negative = 15;
+  if (shared_max_window) *shared_max_window = kSnMaxWindow;
+  if (shared_max_negative) *shared_max_negative = kSnMaxNegative;
+  return W2V_OK;
+}
+
+int w2v_dev_shared_limits(int32_t* max_dim, int32_t* max_window, int32_t* max_negative) {
+  if (max_dim) *max_dim = kSnMaxDim;
+  if (max_window) *max_window = kSnMaxWindow;
+  if (max_negative) *max_negative = kSnMaxNegative;
   return W2V_OK;
 }
 
@@ -378,11 +390,11 @@ int w2v_dev_create(const w2v_dev_config* cfg, w2v_dev** out) {
   if (!cfg || !out) return fail(W2V_ERR_ARG, "w2v_dev_create: null argument");
   *out = nullptr;
   if (cfg->word_dim <= 0) return fail(W2V_ERR_ARG, "word_dim must be > 0");
-  if (cfg->word_dim > kMaxDim) return fail(W2V_ERR_UNSUPPORTED, "word_dim > 2048 unsupported");
+  if (cfg->word_dim > kMaxDim) return fail(W2V_ERR_UNSUPPORTED, "word_dim > " + std::to_string(kMaxDim) + " unsupported");
   if (cfg->window < 0 || cfg->window > kMaxWindowHost)
-    return fail(W2V_ERR_UNSUPPORTED, "window must be in [0, 65535]");
+    return fail(W2V_ERR_UNSUPPORTED, "window must be in [0, " + std::to_string(kMaxWindowHost) + "]");
   if (cfg->negative < 0 || cfg->negative > kMaxNegative)
-    return fail(W2V_ERR_UNSUPPORTED, "negative must be in [0, 65535]");
+    return fail(W2V_ERR_UNSUPPORTED, "negative must be in [0, " + std::to_string(kMaxNegative) + "]");
   if (!cfg->hs && cfg->negative == 0)
     return fail(W2V_ERR_ARG, "neither hs nor negative sampling enabled");
   if (cfg->negative > 0 && cfg->table_size <= 0) return fail(W2V_ERR_ARG, "table_size must be > 0");
@@ -1081,8 +1093,9 @@ constexpr double kSnPressure = 0.06;
 static int check_shared_negatives(const w2v_dev* h, bool at_launch) {
   if (h->cfg.cbow || h->cfg.hs || h->cfg.negative <= 0)
     return fail(W2V_ERR_UNSUPPORTED, "shared negatives: skip-gram with negative sampling only (no hs, no cbow)");
-  if (h->cfg.negative > 15) return fail(W2V_ERR_UNSUPPORTED, "shared negatives: negative must be <= 15");
-  if (h->cfg.window > 8) return fail(W2V_ERR_UNSUPPORTED, "shared negatives: window must be <= 8");
+  if (h->cfg.negative > kSnMaxNegative) return fail(W2V_ERR_UNSUPPORTED, "shared negatives: negative must be <= 15");
+  if (h->cfg.window > kSnMaxWindow) return fail(W2V_ERR_UNSUPPORTED, "shared negatives: window must be <= 8");
+  if (h->cfg.word_dim > kSnMaxDim) return fail(W2V_ERR_UNSUPPORTED, "shared negatives: word_dim must be <= 1024");
   if (at_launch && h->rng != W2V_RNG_PHILOX) return fail(W2V_ERR_UNSUPPORTED, "shared negatives: Philox draws only");
   return W2V_OK;
 }

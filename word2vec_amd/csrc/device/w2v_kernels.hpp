@@ -51,7 +51,9 @@ constexpr int kWave = 64;
 // the private-row flushes, bit 4 the hot context-row atomics of CBOW; in the
 // shared-negatives kernel bit 8 skips the staged atomic rows, bit 16 the
 // private-row flush atomics, bit 32 makes the coherent (sc1) stores plain;
-// bit 64 skips the per-pair kernels' plain (Hogwild) row stores.
+// bit 64 skips the per-pair kernels' plain (Hogwild) row stores, bit 128
+// the LDS adds into the private rows' pending deltas, bit 256 the private
+// rows' pending-delta reads.
 #ifndef W2V_EXP_SKIP
 #define W2V_EXP_SKIP 0
 #endif
@@ -227,7 +229,8 @@ __device__ __forceinline__ uint32_t philox_table_pos(const TrainArgs& a, uint32_
 // ---------------------------------------------------------------------------
 // LDS-privatised rows of the per-pair kernel (when priv_n + ctx_n > 0), per workgroup:
 //   words [0,4) dirty mask of the output rows (2 x 64 bits), [4,8) of the
-//   context rows, [8] centers of the workgroup, [9, 16) unused, then (from
+//   context rows, [8] centers of the workgroup, [9, 13) lock bits of the
+//   output rows, [13, 15) of the context rows (W2V_PRIV_ADD 2), then (from
 //   lds_header_words) the pending deltas: priv_n output rows, then ctx_n
 //   context rows, NV * 64 floats each. The output range holds at most
 //   kPrivMax rows, the context range kCtxMax.
@@ -239,6 +242,7 @@ __host__ __device__ inline int64_t lds_header_words(int64_t, int64_t) { return 1
 struct PrivRows {  // one privatised row range [lo, lo + n) of matrix M (n == 0: none)
   float* delta = nullptr;
   unsigned long long* dirty = nullptr;
+  unsigned* lock = nullptr;  // one bit per row (priv_lock)
   float* M = nullptr;
   int lo = 0;
   int n = 0;
@@ -251,6 +255,7 @@ __device__ __forceinline__ PrivRows out_rows(const TrainArgs& a, float* lds) {
   PrivRows p;
   if (lds == nullptr || a.priv_n == 0) return p;
   p.dirty = reinterpret_cast<unsigned long long*>(lds);
+  p.lock = reinterpret_cast<unsigned*>(lds) + 9;
   p.delta = lds + lds_header_words(a.priv_n, a.ctx_n);
   p.M = const_cast<float*>(a.priv_M);
   p.lo = a.priv_lo;
@@ -263,6 +268,7 @@ __device__ __forceinline__ PrivRows ctx_rows(const TrainArgs& a, float* lds) {
   PrivRows p;
   if (lds == nullptr || a.ctx_n == 0) return p;
   p.dirty = reinterpret_cast<unsigned long long*>(lds + 4);
+  p.lock = reinterpret_cast<unsigned*>(lds) + 13;
   p.delta = lds + lds_header_words(a.priv_n, a.ctx_n) + (int64_t)a.priv_n * (NV * kWave);
   p.M = const_cast<float*>(a.ctx_M);
   p.lo = 0;
@@ -377,20 +383,69 @@ __device__ __forceinline__ void add_to_row(float* M, int64_t row, bool hot, int6
 // A privatised row's value is the global row plus this workgroup's pending delta.
 template <int NV>
 __device__ __forceinline__ void priv_read(const PrivRows& pr, int64_t row, int lane, float (&r)[NV]) {
+  if (W2V_EXP_SKIP & 256) return;
   const float* q = pr.delta + (row - pr.lo) * (NV * kWave) + lane;
 #pragma unroll
   for (int v = 0; v < NV; ++v) r[v] += q[kWave * v];
 }
 
-// ds_add_f32 of delta into the row's pending delta, then mark the row dirty
-// (after the adds: a wave's LDS operations are ordered).
+// Add delta into the row's pending delta, then mark the row dirty (after the
+// adds: a wave's LDS operations are ordered).
+//   W2V_PRIV_ADD 0: ds_add_f32 per element. gfx950 runs an LDS float atomic
+//     one lane at a time: 192 cycles per wave instruction against 4 for
+//     ds_add_u32 and 10.5 for a ds_read + ds_write pair
+//     (tools/lds_atomic_bench.hip, profiles/r05d_lds_atomic_bench.log);
+//     on configs[1] these adds held ~44 % of the kernel's time (a build
+//     without them: 262 -> 468 M words/s, profiles/r05c_*).
+//   1: ds_read + v_add + ds_write, unguarded (timing experiments: two waves
+//     of a workgroup can lose an add, and a flush racing an add counts the
+//     row's delta twice).
+//   2: the same read-modify-write under a per-row LDS lock bit that lane 0
+//     takes with one single-lane ds_or_rtn_b32 (a wave's own LDS operations
+//     execute in order, so the release after the writes publishes them);
+//     flush_private takes the same lock: exact, as the float atomics are.
+#ifndef W2V_PRIV_ADD
+#define W2V_PRIV_ADD 0
+#endif
+__device__ __forceinline__ void priv_lock(const PrivRows& pr, int p, int lane) {
+  unsigned* w = pr.lock + (p >> 5);
+  const unsigned bit = 1u << (p & 31);
+  for (;;) {
+    unsigned old = 0;
+    if (lane == 0) old = atomicOr(w, bit);
+    old = (unsigned)__builtin_amdgcn_readfirstlane((int)old);
+    if (!(old & bit)) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");  // the row's LDS reads stay after the acquire
+}
+__device__ __forceinline__ void priv_unlock(const PrivRows& pr, int p, int lane) {
+  asm volatile("" ::: "memory");  // the row's LDS writes stay before the release
+  if (lane == 0) atomicAnd(pr.lock + (p >> 5), ~(1u << (p & 31)));
+}
 template <int NV>
 __device__ __forceinline__ void priv_add(const PrivRows& pr, int64_t row, int d, int lane, const float (&delta)[NV]) {
   const int64_t p = row - pr.lo;
   float* q = pr.delta + p * (NV * kWave) + lane;
+  if (W2V_PRIV_ADD == 2) {
+    priv_lock(pr, (int)p, lane);
+    float cur[NV];
 #pragma unroll
-  for (int v = 0; v < NV; ++v)
-    if (v < kFullVecs<NV> || lane + kWave * v < d) atomicAdd(q + kWave * v, delta[v]);
+    for (int v = 0; v < NV; ++v) cur[v] = q[kWave * v];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) q[kWave * v] = cur[v] + delta[v];  // padding: 0 + 0
+    priv_unlock(pr, (int)p, lane);
+  } else if (W2V_PRIV_ADD == 1) {
+    float cur[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) cur[v] = q[kWave * v];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) q[kWave * v] = cur[v] + delta[v];  // padding: 0 + 0
+  } else {
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+      if (!(W2V_EXP_SKIP & 128) && (v < kFullVecs<NV> || lane + kWave * v < d)) atomicAdd(q + kWave * v, delta[v]);
+  }
   if (lane == 0) atomicOr(pr.dirty + (p >> 6), 1ull << (p & 63));
 }
 
@@ -416,6 +471,9 @@ __device__ __forceinline__ float ns_sigmoid(float e) { return (float)(1.0 / (dou
 template <bool HSF>
 __device__ __forceinline__ float grad_of(float fl, int cl, float alpha) {
   const float e = expf(-fl);
+#ifdef W2V_HS_F32  // timing experiments only: HS's sigma and g in f32 (not the reference's double)
+  if (HSF) return (1.0f - (float)cl - 1.0f / (1.0f + e)) * alpha;
+#endif
   if (HSF) {
     const float s = (float)(1.0 / (1.0 + (double)e));
     return (float)((1.0 - (double)cl - (double)s) * (double)alpha);
@@ -650,6 +708,20 @@ __device__ __forceinline__ void flush_private(const TrainArgs& a, const PrivRows
     const float sc = pr.ctx ? a.ctx_sc[p & (kCtxMax - 1)] : a.priv_sc[p];
     float* q = pr.delta + p * (NV * kWave) + lane;
     float* dst = pr.M + (pr.lo + p) * a.pitch + lane;
+    if (W2V_PRIV_ADD == 2) {  // take the row under its lock (priv_add)
+      float val[NV];
+      priv_lock(pr, p, lane);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) val[v] = q[kWave * v];
+#pragma unroll
+      for (int v = 0; v < NV; ++v) q[kWave * v] = 0.0f;
+      priv_unlock(pr, p, lane);
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+        if (val[v] != 0.0f && !(W2V_EXP_SKIP & 2))  // 0 past word_dim: skipped
+          (void)__hip_atomic_fetch_add(dst + kWave * v, val[v] * sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      continue;
+    }
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const float val = atomicExch(q + kWave * v, 0.0f);  // 0 past word_dim: skipped

@@ -659,8 +659,11 @@ void Word2Vec::check_limits() const {
   if (word_dim < 1 || word_dim > md) bad("word_dim must be in [1, " + std::to_string(md) + "] on the GPU path");
   if (window < 0 || window > mw) bad("window must be in [0, " + std::to_string(mw) + "] on the GPU path");
   if (negative < 0 || negative > mn) bad("negative must be in [0, " + std::to_string(mn) + "] on the GPU path");
-  if (shared_negatives && (window > smw || negative > smn))
-    bad("shared_negatives needs window <= " + std::to_string(smw) + " and negative <= " + std::to_string(smn));
+  int32_t sdim = 0;
+  (void)w2v_dev_shared_limits(&sdim, nullptr, nullptr);
+  if (shared_negatives && (window > smw || negative > smn || word_dim > sdim))
+    bad("shared_negatives needs window <= " + std::to_string(smw) + ", negative <= " + std::to_string(smn) +
+        " and word_dim <= " + std::to_string(sdim));
   // -1 (auto) or one of the modes w2v_group_set_mode takes; SPLIT / SATURATION
   // need per-row divisors the class does not compute (checked
   // before any replica is created)

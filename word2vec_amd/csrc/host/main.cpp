@@ -153,9 +153,11 @@ int main(int argc, char** argv) {
       std::cout << "Please set -negative <= " << mn << " (the GPU kernels' range)!" << std::endl;
       return 1;
     }
-    if (shared && (window > smw || negative > smn)) {
-      std::cout << "Please set -window <= " << smw << " and -negative <= " << smn << " with -shared-negatives 1!"
-                << std::endl;
+    int32_t sdim = 0;
+    w2v_dev_shared_limits(&sdim, nullptr, nullptr);
+    if (shared && (window > smw || negative > smn || word_dim > sdim)) {
+      std::cout << "Please set -window <= " << smw << ", -negative <= " << smn << " and -size <= " << sdim
+                << " with -shared-negatives 1!" << std::endl;
       return 1;
     }
   }
