@@ -280,6 +280,13 @@ int w2v_dev_set_private_rows(w2v_dev* h, int32_t n);
 int w2v_dev_set_private_rate(w2v_dev* h, float mu);
 /* The rate limit the last parallel launch used (0 = none). Additive. */
 int w2v_dev_private_rate_used(w2v_dev* h, float* mu);
+/* The waves-in-flight cap the last parallel per-pair launch chose for itself
+ * (0: none, or the caller's w2v_dev_set_max_waves). With max_waves 0 a
+ * launch keeps waves x (rows a kept center updates) / V <= 64: past that the
+ * Hogwild staleness of an average row feeds on itself (a 1.8 K-word vocab at
+ * window 150 / negative 80 diverges from 128 waves up, as the reference's own
+ * OpenMP loop does on 8 threads). Every benchmarked shape stays uncapped. */
+int w2v_dev_wave_cap_used(w2v_dev* h, int64_t* waves);
 /* flush_centers: workgroup centers between flushes (0 = auto: 1024 for NS, 64
  * for HS); average_over: the concurrency a private row's summed deltas are
  * scaled down to (default 8; 0 = plain sum). */

@@ -425,30 +425,39 @@ def test_parallel_huge_window_and_many_negatives_run():
 
 
 def test_parallel_huge_window_reference_alpha_full_concurrency():
-    """The r04a input at the reference's alpha 0.025 and full concurrency
-    (window 150, negative 80, V 1,807: each skip-gram center updates ~12 K
-    target rows, every row ~7 times). VERDICT r04 "next" 2: the sequential
-    reference stays finite on it (max |W| 72 with its own draws, 119 with the
-    Philox draws), but the reference's OWN parallel loop does not hold either:
-    its OpenMP Hogwild (Word2Vec.cpp:375-394, the oracle's
+    """The r04a input at the reference's alpha 0.025 with the library's
+    default concurrency (window 150, negative 80, V 1,807: each skip-gram
+    center updates ~12 K target rows, every row ~7 times). VERDICT r04 "next"
+    2. The sequential reference stays finite on it (max |W| 72 with its own
+    draws, 119 with the Philox draws), but the reference's OWN parallel loop
+    does not: its OpenMP Hogwild (Word2Vec.cpp:375-394, the oracle's
     orc_train_omp_shared) reaches max |W| 152 / 1.0e3 / 1.6e5 on 2 / 4 / 8
-    threads (tests/probes/divergence_probe.py, profiles/r05_divergence_oracle.log);
-    the GPU's parallel schedule diverges at every wave count from 128 up and
-    grows to 1e7-1e16 at 32-64 waves (profiles/r05a_1_*, r05b_2_*,
-    r05d_*). So skip-gram must fail LOUDLY there (W2V_ERR_DIVERGED, never
-    silent non-finite weights); CBOW-NS, whose centers update only the
-    negatives' rows of W, trains finite at full concurrency (max |W| 0.54
-    against the sequential 0.96)."""
-    o, d, order = _huge_window_trainer("cbow_ns", 2000, 0.025)
-    st = d.train_epoch(0, order)
-    assert st["words"] == o.samples()[0].size and st["nonfinite"] == 0
-    W, Cm, _ = d.download_model()
-    assert np.isfinite(W).all() and np.isfinite(Cm).all() and np.abs(W).max() < 10.0
-    d.close()
+    threads (tests/probes/divergence_probe.py,
+    profiles/r05_divergence_oracle.log). On the GPU skip-gram's max |W| is 115
+    / 124 / 130 / 142 at 1 / 2 / 4 / 8 waves, 667 at 16, 1e7-1e16 at 32-64 and
+    non-finite from 128 waves up (profiles/r05a_1_*, r05b_2_*, r05d_4_*), so
+    a parallel launch caps its waves in flight by the vocabulary's pressure
+    (effective_max_waves, w2v_dev.hip: here 9; every benchmarked shape stays
+    uncapped) and trains this input to the sequential run's magnitude. An
+    explicit 512-wave launch still diverges, and fails LOUDLY
+    (W2V_ERR_DIVERGED), never with silent non-finite weights."""
+    for mode, wmax in (("cbow_ns", 10.0), ("sg_ns", 400.0)):
+        o, d, order = _huge_window_trainer(mode, 2000, 0.025)
+        st = d.train_epoch(0, order)
+        pol = d.policy()
+        assert st["words"] == o.samples()[0].size and st["nonfinite"] == 0
+        W, Cm, _ = d.download_model()
+        print(f"huge window {mode} alpha 0.025: wave cap {pol['wave_cap']}, max |W| {np.abs(W).max():.3g}")
+        assert np.isfinite(W).all() and np.isfinite(Cm).all() and np.abs(W).max() < wmax
+        # skip-gram: ~12 K rows per center, capped; CBOW-NS: 232, below its 200 sentences' waves
+        assert (0 < pol["wave_cap"] <= 16) if mode == "sg_ns" else pol["wave_cap"] == 0
+        d.close()
     o, d, order = _huge_window_trainer("sg_ns", 2000, 0.025)
+    d.set_max_waves(512)
     with pytest.raises(N.DevError) as e:
         d.train_epoch(0, order)
     assert e.value.code == N.W2V_ERR_DIVERGED
+    assert d.policy()["wave_cap"] == 0  # the caller's cap, not the library's
     d.close()
 
 

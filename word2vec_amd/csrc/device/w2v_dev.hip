@@ -183,6 +183,8 @@ struct w2v_dev {
   bool stats_ok = false;
   double kept_tokens = 0.0;         // expected kept centers of one epoch over the corpus (sum count * min(1, keep))
   std::vector<double> f, fk, node_f, node_fk;
+  double path_len_f = 0.0, path_len_fk = 0.0;  // HS: mean Huffman code length over the tokens / the kept centers
+  int64_t last_wave_cap = 0;        // waves-in-flight cap of the last parallel launch (0: none; effective_max_waves)
   double hot_tau_rows = 0.0;        // automatic hot rows: expected concurrent updates threshold, W / C rows (0 = by vocab, hot_tau_for)
   double hot_tau_nodes = 1.0;       //   ... and Huffman nodes
   double private_rate = -1.0;       // > 0: privatise only rows updated >= this many times per center (private_by_rate);
@@ -237,6 +239,16 @@ static void row_stats(w2v_dev* h) {
       if (h->node_parent[(size_t)j] >= 0) {
         h->node_f[(size_t)h->node_parent[(size_t)j]] += h->node_f[(size_t)j];
         h->node_fk[(size_t)h->node_parent[(size_t)j]] += h->node_fk[(size_t)j];
+      }
+    std::vector<int32_t> depth((size_t)(V - 1), 0);  // the root (V - 2) has depth 0
+    for (int64_t j = V - 3; j >= 0; --j)
+      if (h->node_parent[(size_t)j] > j) depth[(size_t)j] = depth[(size_t)h->node_parent[(size_t)j]] + 1;
+    h->path_len_f = h->path_len_fk = 0.0;
+    for (int64_t w = 0; w < V; ++w)
+      if (h->leaf_node[(size_t)w] >= 0) {
+        const double len = 1.0 + depth[(size_t)h->leaf_node[(size_t)w]];
+        h->path_len_f += h->f[(size_t)w] * len;
+        h->path_len_fk += h->fk[(size_t)w] * len;
       }
   }
 }
@@ -1018,12 +1030,47 @@ static std::pair<int64_t, int64_t> private_by_rate(w2v_dev* h, double mu) {
 // modes; profiles/r03b_small_corpus.log). A launch that fills the chip keeps
 // no limit: there the limit costs 20 % of throughput.
 constexpr double kSmallLaunchRate = 0.1;
-static double private_rate_for(const w2v_dev* h, int64_t count) {
+static double private_rate_for(const w2v_dev* h, int64_t count, int64_t max_waves) {
   if (h->private_rate >= 0.0) return h->private_rate;
   const int64_t per_simd = h->nv <= 2 ? 8 : 4;  // kMinWaves<NV>
   int64_t chip = (int64_t)h->n_cu * 4 * per_simd;
-  if (h->max_waves > 0) chip = std::min(chip, h->max_waves);
+  if (max_waves > 0) chip = std::min(chip, max_waves);
   return count < chip ? kSmallLaunchRate : 0.0;
+}
+
+// Waves in flight of a parallel per-pair launch (max_waves == 0: as many as
+// fit, unless the vocabulary cannot take them). A kept center updates about
+// T rows (skip-gram: its W row and, per context, neg + 1 NS targets and the
+// context's Huffman path; CBOW: the context rows, neg + 1 targets, the
+// center's path), so `waves` concurrent centers update an average row
+// waves x T / V times at once. Past kPairPressure of that the Hogwild
+// staleness feeds on itself: on the r04a input (window 150, negative 80, V
+// 1,807: T ~ 12 K, every row ~7 times per center) skip-gram's max |W| is 115 /
+// 124 / 130 / 142 at 1 / 2 / 4 / 8 waves, 667 at 16, 1e7-1e16 at 32-64 and
+// non-finite from 128 up, against the sequential reference's 72-119
+// (profiles/r05a_1_*, r05b_2_*, r05d_4_divergence_gpu_probe.log) — and the
+// reference's own OpenMP loop reaches 1.6e5 on 8 threads
+// (profiles/r05_divergence_oracle.log). The cap applies only where it is below
+// the waves the launch would run (the chip's, and at most one per sentence of
+// the launch): at 64 it leaves every benchmarked and gated workload as it was
+// (largest: the planted corpus's SG-HS, 3,000 sentences x 66 nodes / 3.4 K
+// rows = 58; configs[0] 4, configs[1] 1.2, configs[2] 0.4) and holds the
+// r04a input's skip-gram at 9 waves.
+constexpr double kPairPressure = 64.0;
+static int64_t effective_max_waves(w2v_dev* h, int64_t count) {
+  if (h->max_waves > 0) return h->max_waves;
+  if (h->sched != W2V_SCHED_PARALLEL || h->update != W2V_UPDATE_PER_PAIR) return 0;
+  row_stats(h);
+  if (!h->stats_ok || h->V < 2) return 0;
+  const double win1 = (double)h->cfg.window + 1.0, neg = (double)h->cfg.negative;
+  const double ns = neg > 0.0 ? neg + 1.0 : 0.0;
+  const double T = h->cfg.cbow ? win1 + ns + (h->cfg.hs ? h->path_len_fk : 0.0)
+                               : 1.0 + win1 * (ns + (h->cfg.hs ? h->path_len_f : 0.0));
+  if (!(T > 0.0)) return 0;
+  const double cap = std::floor(kPairPressure * (double)h->V / T);
+  const int64_t per_simd = h->nv <= 2 ? 8 : 4;  // kMinWaves<NV>
+  const int64_t chip = (int64_t)h->n_cu * 4 * per_simd;
+  return cap < (double)std::min(chip, count) ? std::max<int64_t>(1, (int64_t)cap) : 0;
 }
 
 // Automatic hot rows (hot_rows == W2V_HOT_AUTO): the rows (and Huffman nodes)
@@ -1207,8 +1254,10 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   const int max_wpb = (h->nv <= 6 ? 1024 : 256) / w2v::kWave;
   int wpb = max_wpb;
   if (h->knobs.wpb > 0) wpb = std::min(max_wpb, h->knobs.wpb);  // experiments
-  if (h->max_waves > 0) {
-    int64_t per = h->max_waves / (h->n_cu > 0 ? h->n_cu : 1);
+  const int64_t max_waves = sn_fn ? h->max_waves : effective_max_waves(h, count);
+  h->last_wave_cap = h->max_waves > 0 ? 0 : max_waves;
+  if (max_waves > 0) {
+    int64_t per = max_waves / (h->n_cu > 0 ? h->n_cu : 1);
     wpb = 1;
     while (wpb * 2 <= max_wpb && wpb * 2 <= per) wpb *= 2;
   }
@@ -1251,7 +1300,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     const int64_t avail = hs ? h->V - 1 : h->V;
     if (P > avail) P = avail;
     std::pair<int64_t, int64_t> by_rate{P, w2v::kCtxMax};
-    const double rate = private_rate_for(h, count);
+    const double rate = private_rate_for(h, count, max_waves);
     h->last_private_rate = rate;
     if (rate > 0.0) {
       by_rate = private_by_rate(h, rate);
@@ -1378,7 +1427,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     resident_wg = resident;
     const int64_t need = (count + wpb - 1) / wpb;
     int64_t g = need < resident ? need : resident;
-    if (h->max_waves > 0 && (h->max_waves + wpb - 1) / wpb < g) g = (h->max_waves + wpb - 1) / wpb;
+    if (max_waves > 0 && (max_waves + wpb - 1) / wpb < g) g = (max_waves + wpb - 1) / wpb;
     if (h->knobs.max_blocks > 0 && h->knobs.max_blocks < g) g = h->knobs.max_blocks;  // diagnostics only
     grid = dim3((unsigned)g);
     block = dim3(threads);
@@ -1613,6 +1662,12 @@ int w2v_dev_hot_tau(w2v_dev* h, float* tau_rows, float* tau_nodes) {
 int w2v_dev_private_rate_used(w2v_dev* h, float* mu) {
   if (!h) return fail(W2V_ERR_ARG, "null handle");
   if (mu) *mu = (float)h->last_private_rate;
+  return W2V_OK;
+}
+
+int w2v_dev_wave_cap_used(w2v_dev* h, int64_t* waves) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (waves) *waves = h->last_wave_cap;
   return W2V_OK;
 }
 

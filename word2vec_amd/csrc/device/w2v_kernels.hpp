@@ -391,7 +391,7 @@ __device__ __forceinline__ void priv_read(const PrivRows& pr, int64_t row, int l
 
 // Add delta into the row's pending delta, then mark the row dirty (after the
 // adds: a wave's LDS operations are ordered).
-//   W2V_PRIV_ADD 0: ds_add_f32 per element. gfx950 runs an LDS float atomic
+//   W2V_PRIV_ADD 0 (rounds 1-4): ds_add_f32 per element. gfx950 runs an LDS float atomic
 //     one lane at a time: 192 cycles per wave instruction against 4 for
 //     ds_add_u32 and 10.5 for a ds_read + ds_write pair
 //     (tools/lds_atomic_bench.hip, profiles/r05d_lds_atomic_bench.log);
@@ -400,12 +400,15 @@ __device__ __forceinline__ void priv_read(const PrivRows& pr, int64_t row, int l
 //   1: ds_read + v_add + ds_write, unguarded (timing experiments: two waves
 //     of a workgroup can lose an add, and a flush racing an add counts the
 //     row's delta twice).
-//   2: the same read-modify-write under a per-row LDS lock bit that lane 0
-//     takes with one single-lane ds_or_rtn_b32 (a wave's own LDS operations
-//     execute in order, so the release after the writes publishes them);
-//     flush_private takes the same lock: exact, as the float atomics are.
-#ifndef W2V_PRIV_ADD
-#define W2V_PRIV_ADD 0
+//   2 (the default): the same read-modify-write under a per-row LDS lock bit
+//     that lane 0 takes with one single-lane ds_or_rtn_b32 (a wave's own LDS
+//     operations execute in order, so the release after the writes publishes
+//     them); flush_private takes the same lock: exact, as the float atomics
+//     are. Same box, alternating (profiles/r05e_*): configs[1] 262 -> 330-337
+//     M words/s (unguarded 334-337), configs[0] / [2] unchanged, every
+//     headline-scale and full-concurrency quality gate passing.
+#ifndef W2V_PRIV_ADD  // 2 since round 5: configs[1] 262 -> 330-337 M words/s (profiles/r05e_2_ab_c2_lock.log)
+#define W2V_PRIV_ADD 2
 #endif
 __device__ __forceinline__ void priv_lock(const PrivRows& pr, int p, int lane) {
   unsigned* w = pr.lock + (p >> 5);

@@ -234,9 +234,11 @@ class DeviceTrainer:
         self._chk(self.lib.w2v_dev_hot_tau(self.h, C.byref(tr), C.byref(tn)), "w2v_dev_hot_tau")
         mu = C.c_float()
         self._chk(self.lib.w2v_dev_private_rate_used(self.h, C.byref(mu)), "w2v_dev_private_rate_used")
+        wc = C.c_int64()
+        self._chk(self.lib.w2v_dev_wave_cap_used(self.h, C.byref(wc)), "w2v_dev_wave_cap_used")
         return {"hot_rows": r.value, "hot_nodes": n.value, "private_rows": p.value, "context_rows": c.value,
                 "flush_centers": f.value, "context_flush": cf.value, "hot_tau_rows": tr.value,
-                "private_rate": round(mu.value, 4)}
+                "private_rate": round(mu.value, 4), "wave_cap": wc.value}
 
     def set_private_rows(self, n: int):
         """Hottest output rows privatised per workgroup in LDS: -1 auto (default), 0 off."""
