@@ -1180,23 +1180,34 @@ int w2v_dev_train_sentences_async(w2v_dev* h, int32_t epoch, const int64_t* orde
 }
 
 // Flush interval of the HS privatised rows (auto: flush_centers == 0), in
-// centers of a workgroup: the fewest of 64, 128, 256 that still gives every
-// workgroup at least kHsFlushes flushes per launch (expected kept centers of
-// the launch / its workgroups, from the corpus statistics). Staleness is the
-// model change between flushes, i.e. the launch's fraction between them: a
-// long launch (configs[1]: ~36 K centers per workgroup) can flush less often
-// with the same fraction, a short one (a small corpus, a replica's slice)
-// keeps 64. Measured on configs[1]: 64 / 128 / 256 (context rows at half) run
-// 152 / 1xx / 171 M words/s; the planted corpus (~2.4 K centers per
-// workgroup, stays at 64) loses 3-5 similarity points when forced to 256
-// (profiles/r02u_c2_flush_hotnode_grid_and_quality.log, r02z_*).
-constexpr double kHsFlushes = 128.0;
+// centers of a workgroup: the fewest of 64, 128, ..., 1024 that still gives
+// every workgroup at least kHsFlushes flushes per launch (expected kept
+// centers of the launch / its workgroups, from the corpus statistics); the
+// context rows flush at half of it. Staleness is the model change between
+// flushes, i.e. the launch's fraction between them: a long launch can flush
+// less often with the same fraction, a short one (a small corpus, a
+// replica's slice) keeps 64.
+// Round 2 set 128 flushes per workgroup and a 256 cap (configs[1] 152 -> 173
+// M words/s; the planted corpus lost 3-5 similarity points when forced to
+// 256). Round 5, with the private rows' LDS adds no longer the bottleneck
+// (W2V_PRIV_ADD), the flush atomics and the rows' write traffic are: configs[1]
+// at 256 / 128 / 512 / 1024 node-interval (context at half) runs 331-341 /
+// 426 / 443 M words/s (profiles/r05i_1_*, r05j_1_ab_c2_flush.log), its
+// headline-scale paired gate +13.3 / +6.3, +16.4 / +6.3, +13.5 / +2.5
+// (analogy / similarity against the sequential oracle, r05j_2_*); the
+// text8-like corpus at 512 / 256: +20.0..+26.8 / +13.0..+14.1 as at 256 / 128
+// (r05j_3_*), text8_small at 256 / 128: +25.6 / +19.5 (r05j_4_*). So 32
+// flushes per workgroup and a 1024 cap: configs[1] (~33 K kept centers per
+// workgroup) takes 1024 / 512, the text8-like corpus 512 / 256, text8_small
+// 256 / 128, the planted corpus (~2.4 K per workgroup) keeps 64 / 32.
+constexpr double kHsFlushes = 32.0;
+constexpr int32_t kHsFlushMax = 1024;
 static int32_t auto_hs_flush(w2v_dev* h, int64_t count, int64_t G) {
   row_stats(h);
   if (!h->stats_ok || h->n_sent <= 0 || G <= 0) return 64;
   const double cpw = h->kept_tokens * ((double)count / (double)h->n_sent) / (double)G;
   int32_t fe = 64;
-  while (fe < 256 && 2.0 * fe * kHsFlushes <= cpw) fe *= 2;
+  while (fe < kHsFlushMax && 2.0 * fe * kHsFlushes <= cpw) fe *= 2;
   return fe;
 }
 
