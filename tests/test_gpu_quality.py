@@ -241,10 +241,14 @@ def test_quality_shared_negatives_c5_hyperparameters():
 # frequent rows), configs[1] CBOW-HS +13.66 / +6.34 (per seed +13.40..+13.91 /
 # +6.02..+6.67), configs[0] similarity +3.28 / +3.29 — the high bound is that
 # mean + 1. A policy change that moves a score past it fails here and is
-# explained in DESIGN.md §2 before the bound moves.
+# explained in DESIGN.md §2 before the bound moves. Moved once, round 5:
+# configs[1]'s HS flush interval went from 256 / 128 to 512 / 256 centers
+# (auto_hs_flush, w2v_dev.hip: 331 -> 420-426 M words/s) and its analogy
+# from +13.3..+13.7 to +16.4 / +17.3 (profiles/r05j_2_*, r05k_tests.log;
+# similarity unchanged at +6.3 / +6.45): analogy high 18.4.
 HEADLINE_BOUNDS = {
     "c3": {"analogy": (-1.0, 3.1), "similarity": (-1.0, 1.0)},
-    "c2": {"analogy": (-1.0, 14.7), "similarity": (-1.0, 7.4)},
+    "c2": {"analogy": (-1.0, 18.4), "similarity": (-1.0, 7.4)},
     "c1": {"analogy": (-1.0, 1.0), "similarity": (-1.0, 4.3)},
 }
 

@@ -1197,9 +1197,11 @@ int w2v_dev_train_sentences_async(w2v_dev* h, int32_t epoch, const int64_t* orde
 // (analogy / similarity against the sequential oracle, r05j_2_*); the
 // text8-like corpus at 512 / 256: +20.0..+26.8 / +13.0..+14.1 as at 256 / 128
 // (r05j_3_*), text8_small at 256 / 128: +25.6 / +19.5 (r05j_4_*). So 32
-// flushes per workgroup and a 1024 cap: configs[1] (~33 K kept centers per
-// workgroup) takes 1024 / 512, the text8-like corpus 512 / 256, text8_small
-// 256 / 128, the planted corpus (~2.4 K per workgroup) keeps 64 / 32.
+// flushes per workgroup and a 1024 cap: configs[1] (25 K kept centers per
+// workgroup) takes 512 / 256 (420-426 M words/s; its headline-scale gate
+// +16.4..+17.3 / +6.3..+6.45, profiles/r05k_tests.log), the text8-like corpus
+// (32 K) 512 / 256, text8_small (13 K) 256 / 128, the planted corpus (2.4 K)
+// keeps 64 / 32 (every paired gate unchanged, r05k_tests.log).
 constexpr double kHsFlushes = 32.0;
 constexpr int32_t kHsFlushMax = 1024;
 static int32_t auto_hs_flush(w2v_dev* h, int64_t count, int64_t G) {
