@@ -255,9 +255,9 @@ def test_quality_shared_negatives_c5_hyperparameters():
 # mean + 1. A policy change that moves a score past it fails here and is
 # explained in DESIGN.md §2 before the bound moves. Moved once, round 5:
 # configs[1]'s HS flush interval went from 256 / 128 to 512 / 256 centers
-# (auto_hs_flush, w2v_dev.hip: 331 -> 420-426 M words/s) and its analogy
-# from +13.3..+13.7 to +16.4 / +17.3 (profiles/r05j_2_*, r05k_tests.log;
-# similarity unchanged at +6.3 / +6.45): analogy high 18.4.
+# (auto_hs_flush, w2v_dev.hip: 331 -> 420-428 M words/s) and its analogy
+# from +13.1..+13.7 (five leases) to +16.4 / +17.3 (profiles/r05j_2_*,
+# r05k_tests.log; similarity unchanged at +6.3 / +6.45): analogy high 18.4.
 HEADLINE_BOUNDS = {
     "c3": {"analogy": (-1.0, 3.1), "similarity": (-1.0, 1.0)},
     "c2": {"analogy": (-1.0, 18.4), "similarity": (-1.0, 7.4)},

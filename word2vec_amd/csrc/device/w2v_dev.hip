@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -112,7 +113,7 @@ static Knobs read_knobs() {
 struct CorpusBuf {
   int32_t* ids = nullptr;
   int64_t* soff = nullptr;
-  int refs = 1;
+  std::atomic<int> refs{1};  // handles on different host threads may share one corpus
 };
 
 struct w2v_dev {
@@ -1194,14 +1195,15 @@ int w2v_dev_train_sentences_async(w2v_dev* h, int32_t epoch, const int64_t* orde
 // at 256 / 128 / 512 / 1024 node-interval (context at half) runs 331-341 /
 // 426 / 443 M words/s (profiles/r05i_1_*, r05j_1_ab_c2_flush.log), its
 // headline-scale paired gate +13.3 / +6.3, +16.4 / +6.3, +13.5 / +2.5
-// (analogy / similarity against the sequential oracle, r05j_2_*); the
-// text8-like corpus at 512 / 256: +20.0..+26.8 / +13.0..+14.1 as at 256 / 128
-// (r05j_3_*), text8_small at 256 / 128: +25.6 / +19.5 (r05j_4_*). So 32
-// flushes per workgroup and a 1024 cap: configs[1] (25 K kept centers per
-// workgroup) takes 512 / 256 (420-426 M words/s; its headline-scale gate
-// +16.4..+17.3 / +6.3..+6.45, profiles/r05k_tests.log), the text8-like corpus
-// (32 K) 512 / 256, text8_small (13 K) 256 / 128, the planted corpus (2.4 K)
-// keeps 64 / 32 (every paired gate unchanged, r05k_tests.log).
+// (analogy / similarity against the sequential oracle, r05j_2_*): 1024 / 512
+// is the fastest, but not reproducible: the same gate ran +19.3 / +6.0 in the
+// next lease (both seeds moved together, profiles/r05n_tests_*), where 256 /
+// 128 held +13.1..+13.7 / +5.2..+6.5 over five leases and 512 / 256 +16.4 /
+// +6.3 and +17.3 / +6.45 over two. So 32 flushes per workgroup and a 1024
+// cap: configs[1] (25 K kept centers per workgroup) and the text8-like corpus
+// (32 K) take 512 / 256 (text8-like there: +20.0..+26.8 / +13.0..+14.1, as at
+// 128 / 64, r05j_3_*), text8_small (13 K) 256 / 128 (+25.6 / +19.5,
+// r05j_4_*), the planted corpus (2.4 K) keeps 64 / 32.
 constexpr double kHsFlushes = 32.0;
 constexpr int32_t kHsFlushMax = 1024;
 static int32_t auto_hs_flush(w2v_dev* h, int64_t count, int64_t G) {
