@@ -943,6 +943,18 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
 //   SG-HS nodes            (window + 1) sum_{w below} f(w)   every context's path (:342-345)
 //   CBOW-HS nodes          sum_{w below} fk(w)               the center's path (:304-306)
 //   CBOW context (C) rows  (window + 1) f(r)                 window positions (:288-300)
+// NS output rows 64..127 of the private range (private_rows > 64, or
+// automatically on skip-gram NS with V >= kWidePrivVocab) flush their deltas
+// scaled to at most kPrivTailAverage concurrent contributions instead of the
+// top rows' 8: with 128 private rows (profiles/r05p_*: W2V_PRIV_TAIL_AVG 24 /
+// 40 / 48) configs[0]'s paired gate is -0.02 / -0.61 / -1.60 analogy and the
+// text8-like corpus's -9.1 / -0.21 / +1.28 similarity (the averaged flush
+// damps rows 64..127 less at 40), configs[2]'s +1.40 / -0.16 at 40. Only the
+// large-vocabulary rule (kWidePrivVocab) ships 128 rows by default: at 40 the
+// text8-shaped corpora sit within a point of both gates, too thin a margin.
+constexpr double kPrivTailAverage = 40.0;
+constexpr int64_t kWidePrivVocab = 500000;
+
 static void priv_scales(w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool shared) {
   for (int p = 0; p < w2v::kPrivMax; ++p) a.priv_sc[p] = 1.0f;
   for (int p = 0; p < w2v::kCtxMax; ++p) a.ctx_sc[p] = 1.0f;
@@ -972,7 +984,7 @@ static void priv_scales(w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool shared) {
       for (int p = 0; p < a.priv_n; ++p) {
         const int64_t r = a.priv_lo + p;
         const double m = (shared || cbow) ? fk(r) + neg * u(r) : win1 * (f(r) + neg * u(r));
-        const double avg = (p >= 64 && h->knobs.priv_tail_avg >= 0.0) ? h->knobs.priv_tail_avg : S;  // experiments
+        const double avg = p < 64 ? S : h->knobs.priv_tail_avg >= 0.0 ? h->knobs.priv_tail_avg : kPrivTailAverage;
         a.priv_sc[p] = sc(m, a.flush_every, avg);
       }
     }
@@ -1308,8 +1320,14 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     int64_t fit = budget / row_bytes;
     // <= 64 output rows by default: 128 (kPrivMax) cost 12 points of
     // text8-like similarity on SG-NS (the averaged flush under-trains the
-    // less contended rows 64..127); an explicit private_rows may ask for more
-    int64_t P = std::min<int64_t>(fit, h->private_rows > 0 ? w2v::kPrivMax : 64);
+    // less contended rows 64..127); an explicit private_rows may ask for more.
+    // Skip-gram NS on a large vocabulary (>= kWidePrivVocab) takes up to 128,
+    // rows 64..127 flushed with the gentler kPrivTailAverage (priv_scales):
+    // there rows 64..127 are function words a 50 M-token launch moves
+    // constantly, in a 70-100 K vocabulary they are evaluation words
+    // (text8: "world", "city", "states", "war").
+    const bool wide_priv = !h->cfg.cbow && !h->cfg.hs && h->V >= kWidePrivVocab;
+    int64_t P = std::min<int64_t>(fit, (h->private_rows > 0 || wide_priv) ? w2v::kPrivMax : 64);
     if (h->private_rows >= 0) P = std::min<int64_t>(P, h->private_rows);
     const bool hs = h->cfg.hs != 0;
     const int64_t avail = hs ? h->V - 1 : h->V;
