@@ -952,8 +952,12 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
 // damps rows 64..127 less at 40), configs[2]'s +1.40 / -0.16 at 40. Only the
 // large-vocabulary rule (kWidePrivVocab) ships 128 rows by default: at 40 the
 // text8-shaped corpora sit within a point of both gates, too thin a margin.
+// Smaller skip-gram NS vocabularies privatise kSgNsPrivRows = 96 (r05r: 96 /
+// 112 rows, configs[0] +0.02 / -0.27 analogy, text8-like similarity +0.77..
+// +2.08 / -0.54..+0.52 at 40; configs[0] 316 -> 357 / 374 M words/s).
 constexpr double kPrivTailAverage = 40.0;
 constexpr int64_t kWidePrivVocab = 500000;
+constexpr int64_t kSgNsPrivRows = 96;
 
 static void priv_scales(w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool shared) {
   for (int p = 0; p < w2v::kPrivMax; ++p) a.priv_sc[p] = 1.0f;
@@ -1318,16 +1322,18 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     const int64_t budget =
         std::min<int64_t>(160 * 1024, per_wave * (int64_t)wpb) - 4 * w2v::lds_header_words(w2v::kPrivMax, 64);
     int64_t fit = budget / row_bytes;
-    // <= 64 output rows by default: 128 (kPrivMax) cost 12 points of
-    // text8-like similarity on SG-NS (the averaged flush under-trains the
-    // less contended rows 64..127); an explicit private_rows may ask for more.
-    // Skip-gram NS on a large vocabulary (>= kWidePrivVocab) takes up to 128,
-    // rows 64..127 flushed with the gentler kPrivTailAverage (priv_scales):
-    // there rows 64..127 are function words a 50 M-token launch moves
-    // constantly, in a 70-100 K vocabulary they are evaluation words
-    // (text8: "world", "city", "states", "war").
-    const bool wide_priv = !h->cfg.cbow && !h->cfg.hs && h->V >= kWidePrivVocab;
-    int64_t P = std::min<int64_t>(fit, (h->private_rows > 0 || wide_priv) ? w2v::kPrivMax : 64);
+    // <= 64 output rows by default for CBOW and HS. Skip-gram NS takes
+    // kSgNsPrivRows (96), on a large vocabulary (>= kWidePrivVocab) up to 128,
+    // rows past the 64th flushed with the gentler kPrivTailAverage
+    // (priv_scales): 128 at the top rows' average cost 12 points of text8-like
+    // similarity (the averaged flush under-trains the less contended rows);
+    // at V >= 500 K rows 64..127 are function words a 50 M-token launch moves
+    // constantly, in a 70-100 K vocabulary rows 96..127 are evaluation words
+    // (text8: "world", "city", "states", "war"). An explicit private_rows may
+    // ask for up to kPrivMax.
+    const bool sg_ns = !h->cfg.cbow && !h->cfg.hs;
+    const int64_t auto_rows = !sg_ns ? 64 : h->V >= kWidePrivVocab ? w2v::kPrivMax : kSgNsPrivRows;
+    int64_t P = std::min<int64_t>(fit, h->private_rows > 0 ? w2v::kPrivMax : auto_rows);
     if (h->private_rows >= 0) P = std::min<int64_t>(P, h->private_rows);
     const bool hs = h->cfg.hs != 0;
     const int64_t avail = hs ? h->V - 1 : h->V;
