@@ -258,9 +258,12 @@ def test_quality_shared_negatives_c5_hyperparameters():
 # (auto_hs_flush, w2v_dev.hip: 331 -> 420-428 M words/s) and its analogy
 # from +13.1..+13.7 (five leases) to +16.4 / +17.3 (profiles/r05j_2_*,
 # r05k_tests.log; similarity unchanged at +6.3 / +6.45): analogy high 18.4.
+# With that policy unchanged, four whole-suite runs then spread +14.0..+17.8 /
+# +4.3..+6.47 (r05k, r05n, r05o, r05s_tests.log): high = the largest + 2 /
+# + 1.5, so the run-to-run spread of one policy does not decide the gate.
 HEADLINE_BOUNDS = {
     "c3": {"analogy": (-1.0, 3.1), "similarity": (-1.0, 1.0)},
-    "c2": {"analogy": (-1.0, 18.4), "similarity": (-1.0, 7.4)},
+    "c2": {"analogy": (-1.0, 19.8), "similarity": (-1.0, 8.0)},
     "c1": {"analogy": (-1.0, 1.0), "similarity": (-1.0, 4.3)},
 }
 
