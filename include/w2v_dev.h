@@ -262,19 +262,25 @@ int w2v_dev_hot_tau(w2v_dev* h, float* tau_rows, float* tau_nodes);
 int w2v_dev_policy(w2v_dev* h, int64_t* hot_rows, int64_t* hot_nodes, int32_t* private_rows, int32_t* context_rows);
 /* The flush intervals (workgroup centers) of the LDS-private output and
  * context rows the last parallel launch used (0 = that range was empty).
- * Auto for HS: the fewest of 64 / 128 / 256 that still gives every workgroup
- * >= 128 flushes per launch (context rows at half). Additive; no reference
- * counterpart. */
+ * Auto for HS: the fewest of 64 ... 1024 that still gives every workgroup
+ * >= 32 flushes per launch (context rows at half); NS: 1024. Additive; no
+ * reference counterpart. */
 int w2v_dev_flush_policy(w2v_dev* h, int32_t* flush_centers, int32_t* context_flush);
 /* Expected updates per raw corpus token of every row of matrix `which` (0 W,
  * 1 C, 2 synapses1; n = its row count), from the uploaded vocab and corpus
  * statistics: what the flush scales, the hot-row threshold and the replica
  * exchange's per-row divisors are computed from. Additive. */
 int w2v_dev_row_update_rates(w2v_dev* h, int32_t which, double* out, int64_t n);
+/* LDS-private output rows per workgroup (-1, the default = automatic: as
+ * many as fit the LDS budget, at most 64 for CBOW and HS, 96 for skip-gram NS,
+ * 128 for skip-gram NS on a vocabulary >= 500 K words; rows past the 64th
+ * flush with a gentler average). n > 0 asks for up to 128;
+ * 0 disables them. Additive; no reference counterpart. */
 int w2v_dev_set_private_rows(w2v_dev* h, int32_t n);
 /* With private_rows = -1: privatise only the rows (Huffman nodes for HS, and
  * CBOW context rows) a center updates at least `mu` times on average, from
- * the corpus statistics (0 = no rate limit: as many as fit, <= 64; -1, the
+ * the corpus statistics (0 = no rate limit: as many as fit, up to the
+ * automatic count of w2v_dev_set_private_rows; -1, the
  * default = 0.1 for a launch with fewer sentences than the chip holds waves,
  * else no limit). */
 int w2v_dev_set_private_rate(w2v_dev* h, float mu);
