@@ -82,6 +82,7 @@ struct Knobs {
   int scale_resident = 0;        // W2V_SCALE_RESIDENT=1: flush scales from the chip's resident workgroups, not the launch's grid
   double priv_tail_avg = -1;     // W2V_PRIV_TAIL_AVG: private_average of the NS output rows past the 64th (0 = plain sum)
   int sn_per_cu = 0;             // W2V_SN_PER_CU: shared-negatives workgroups per CU (cap)
+  double ctx_avg = -1;           // W2V_CTX_AVG: private_average of the CBOW context rows (0 = plain sum)
   std::string desc;             // "NAME=value ..." of the variables that were set
 };
 
@@ -102,6 +103,7 @@ static Knobs read_knobs() {
   if (const char* v = get("W2V_SCALE_RESIDENT")) k.scale_resident = std::atoi(v) != 0;
   if (const char* v = get("W2V_PRIV_TAIL_AVG")) k.priv_tail_avg = std::max(0.0, std::atof(v));
   if (const char* v = get("W2V_SN_PER_CU")) k.sn_per_cu = std::max(0, std::atoi(v));
+  if (const char* v = get("W2V_CTX_AVG")) k.ctx_avg = std::max(0.0, std::atof(v));
   return k;
 }
 
@@ -993,7 +995,8 @@ static void priv_scales(w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool shared) {
       }
     }
   }
-  for (int p = 0; p < a.ctx_n; ++p) a.ctx_sc[p] = sc(win1 * f(p), a.ctx_flush_every, S);
+  const double Sc = h->knobs.ctx_avg >= 0.0 ? h->knobs.ctx_avg : S;
+  for (int p = 0; p < a.ctx_n; ++p) a.ctx_sc[p] = sc(win1 * f(p), a.ctx_flush_every, Sc);
 }
 
 // Privatised rows by update rate (private_rate mu > 0, private_rows = -1): only
