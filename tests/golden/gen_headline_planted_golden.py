@@ -13,6 +13,7 @@ parallel schedule and update policy are the only difference.
        at min_count 5, 256 K types, the most frequent word 5 % of tokens
        (text8: 71.3 K, 254 K, 6 %)
   c1   configs[0]: SG-NS neg 5 d100 on the same text8-shaped corpus
+  c2ns the reference's CBOW-NS mode (neg 5, d200) on configs[1]'s corpus
 
 usage (repo root): python tests/golden/gen_headline_planted_golden.py c3 [seeds]
   -> tests/golden/quality_headline_<workload>_oracle.json (one record per seed).
@@ -34,6 +35,8 @@ WORKLOADS = {
                negative=5, alpha=0.025),
     "c2": dict(corpus=TEXT8, mode="cbow_hs", dim=200, negative=0, alpha=0.05),
     "c1": dict(corpus=TEXT8, mode="sg_ns", dim=100, negative=5, alpha=0.025),
+    # the reference's CBOW-NS mode (no BASELINE config of its own) on configs[1]'s corpus and width
+    "c2ns": dict(corpus=TEXT8, mode="cbow_ns", dim=200, negative=5, alpha=0.05),
 }
 TRAIN = dict(window=5, iters=1, table_size=100_000_000, min_count=5, subsample=1e-4)
 SEEDS = (1, 2)

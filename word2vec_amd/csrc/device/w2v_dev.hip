@@ -995,7 +995,9 @@ static void priv_scales(w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool shared) {
       }
     }
   }
-  const double Sc = h->knobs.ctx_avg >= 0.0 ? h->knobs.ctx_avg : S;
+  // CBOW context rows: HS averages them like its nodes; NS adds the plain sum
+  // (round 5; launch_train has the measurements): at any average their flush loses CBOW-NS's similarity.
+  const double Sc = h->knobs.ctx_avg >= 0.0 ? h->knobs.ctx_avg : h->cfg.hs ? S : 0.0;
   for (int p = 0; p < a.ctx_n; ++p) a.ctx_sc[p] = sc(win1 * f(p), a.ctx_flush_every, Sc);
 }
 
@@ -1353,12 +1355,16 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
       a.priv_lo = (int32_t)(hs ? avail - P : 0);  // HS: the P internal nodes nearest the root (V-2)
       a.priv_n = (int32_t)P;
     }
-    // Auto: CBOW-HS only. It doubles CBOW-HS throughput and raises its planted-
-    // corpus scores; for CBOW-NS (hot rows privatised on both sides of every
-    // dot product) it fails the similarity gate at every flush interval tried
-    // (profiles/r01_context_rows.log).
+    // Auto for CBOW. It doubles CBOW-HS throughput and raises its planted-
+    // corpus scores. CBOW-NS (hot rows privatised on both sides of every dot
+    // product) failed the similarity gate at every flush interval while its
+    // context rows were averaged like the output rows (profiles/r01_context_rows.log;
+    // round 5, 8 averaged contributions at 256 / 64 / 32 / 16 centers: planted
+    // similarity -45 / -37 / -20 / -2.6, r05t_2_*); flushed as a plain sum
+    // (priv_scales) it is within a point of the oracle at 256 (+0.9 / +0.2,
+    // r05u_3_*) and runs 4.6x the atomic context rows on configs[2]'s corpus
+    // (50.8 -> 232 M words/s, r05t_1_*).
     int64_t Q = h->cfg.cbow ? std::min<int64_t>({fit - P, (int64_t)w2v::kCtxMax, h->V}) : 0;
-    if (h->context_rows < 0 && !h->cfg.hs) Q = 0;
     if (h->context_rows >= 0) Q = std::min<int64_t>(Q, h->context_rows);
     else if (rate > 0.0) Q = std::min(Q, by_rate.second);
     if (Q > 0) {
