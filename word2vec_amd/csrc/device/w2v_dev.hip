@@ -960,6 +960,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
 constexpr double kPrivTailAverage = 40.0;
 constexpr int64_t kWidePrivVocab = 500000;
 constexpr int64_t kSgNsPrivRows = 96;
+constexpr double kCtxAvgNs = 128.0;
 
 static void priv_scales(w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool shared) {
   for (int p = 0; p < w2v::kPrivMax; ++p) a.priv_sc[p] = 1.0f;
@@ -995,9 +996,9 @@ static void priv_scales(w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool shared) {
       }
     }
   }
-  // CBOW context rows: HS averages them like its nodes; NS adds the plain sum
-  // (round 5; launch_train has the measurements): at any average their flush loses CBOW-NS's similarity.
-  const double Sc = h->knobs.ctx_avg >= 0.0 ? h->knobs.ctx_avg : h->cfg.hs ? S : 0.0;
+  // CBOW context rows: HS averages them like its nodes (S); NS at up to
+  // kCtxAvgNs contributions (launch_train has the measurements).
+  const double Sc = h->knobs.ctx_avg >= 0.0 ? h->knobs.ctx_avg : h->cfg.hs ? S : kCtxAvgNs;
   for (int p = 0; p < a.ctx_n; ++p) a.ctx_sc[p] = sc(win1 * f(p), a.ctx_flush_every, Sc);
 }
 
@@ -1360,10 +1361,14 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     // product) failed the similarity gate at every flush interval while its
     // context rows were averaged like the output rows (profiles/r01_context_rows.log;
     // round 5, 8 averaged contributions at 256 / 64 / 32 / 16 centers: planted
-    // similarity -45 / -37 / -20 / -2.6, r05t_2_*); flushed as a plain sum
-    // (priv_scales) it is within a point of the oracle at 256 (+0.9 / +0.2,
-    // r05u_3_*) and runs 4.6x the atomic context rows on configs[2]'s corpus
-    // (50.8 -> 232 M words/s, r05t_1_*).
+    // similarity -45 / -37 / -20 / -2.6, r05t_2_*). With up to kCtxAvgNs = 128
+    // contributions (priv_scales) at 256 centers it scores as the atomic context
+    // rows do: planted +2.6 / +0.2 (r05u_2_*), configs[1]'s corpus +3.0..+3.5 /
+    // +3.0..+3.6 against +3.2..+3.7 / +3.2..+3.4 (three runs each,
+    // r05w_*_policy_probe.log); 32 / 64 over-train the planted analogy (+41 / +21),
+    // a plain sum is noisy there (per seed -4.4..+5.3 similarity). It runs 4.6x
+    // the atomic context rows on configs[2]'s corpus (50.5 -> 232 M words/s)
+    // and 5.8x on configs[1]'s at d200 / negative 5 (106 -> 613 M; r05v_2_*, r05v_3_*).
     int64_t Q = h->cfg.cbow ? std::min<int64_t>({fit - P, (int64_t)w2v::kCtxMax, h->V}) : 0;
     if (h->context_rows >= 0) Q = std::min<int64_t>(Q, h->context_rows);
     else if (rate > 0.0) Q = std::min(Q, by_rate.second);
