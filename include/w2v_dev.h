@@ -300,10 +300,11 @@ int w2v_dev_set_private_sync(w2v_dev* h, int32_t flush_centers, float average_ov
 /* CBOW only: privatise the `rows` hottest context rows of C (a window's
  * contexts are not subsampled, Word2Vec.cpp:286-300, so the most frequent
  * words sit in most windows) in LDS as well, beside the output rows, flushed
- * every flush_centers workgroup centers with the same averaging. rows: -1 =
- * auto (CBOW-HS: as many as fit beside the output rows, at most 64; CBOW-NS:
- * none); 0 = off (those rows then take the hot-row
- * atomics). flush_centers: 0 = auto (32 for HS, 256 for NS). */
+ * every flush_centers workgroup centers, scaled to at most 8 (CBOW-HS, the
+ * output rows' average) or 128 (CBOW-NS) concurrent contributions. rows: -1 =
+ * auto (as many as fit beside the output rows, at most 64);
+ * 0 = off (those rows then take the hot-row atomics). flush_centers: 0 =
+ * auto (HS: half the output rows' interval; NS: 256). */
 int w2v_dev_set_context_private(w2v_dev* h, int32_t rows, int32_t flush_centers);
 /* Cap on wavefronts in flight in the parallel schedule (0 = as many as fit,
  * the default). Fewer wavefronts, less staleness, less throughput. */
