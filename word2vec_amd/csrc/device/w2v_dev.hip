@@ -961,6 +961,7 @@ constexpr double kPrivTailAverage = 40.0;
 constexpr int64_t kWidePrivVocab = 500000;
 constexpr int64_t kSgNsPrivRows = 96;
 constexpr double kCtxAvgNs = 128.0;
+constexpr int64_t kSnPrivRowsWide = 4;  // shared negatives above negative 5 (launch_train)
 
 static void priv_scales(w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool shared) {
   for (int p = 0; p < w2v::kPrivMax; ++p) a.priv_sc[p] = 1.0f;
@@ -1400,11 +1401,18 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     // three times as stale, and the averaged flush costs the text8-like gate 8
     // similarity points (90.7-91.6 / 62.8-65.1 with 2-32 averaged contributions
     // against 98.1 / 72.2 with no private rows, the sequential minibatch
-    // scoring 98.3 / 69.7: profiles/r03q_c5_*.log), so the automatic setting
-    // keeps no private rows above negative 5 (their slots stage atomic rows).
+    // scoring 98.3 / 69.7: profiles/r03q_c5_*.log). Round 5 (configs[4]'s
+    // paired gate against the sequential minibatch, 3 seeds per run): 10 rows
+    // fail at every average (1-8: -0.9..-2.1 / -1.7..-5.4; 128 and the plain
+    // sum diverge), 2 / 4 / 6 rows at 4 or 8 pass in every run (4 at 8: +0.16..
+    // +0.45 / +0.27..+1.06 in three; at 4: -0.01..+0.26 / -0.67..+1.30 in five;
+    // the configuration without them +0.04..+0.34 / -0.71..+0.84) and run
+    // 71.7 / 73.2 / 74.0 M words/s against 66.7 M (profiles/r05y_*, r05z_*,
+    // r05aa_*). Above negative 5 the automatic setting keeps 4 private rows
+    // (the other slots stage atomic rows).
     {
       const int64_t slots = std::min<int64_t>(32, w2v::kSnPrivBytes / (h->pitch * (int64_t)sizeof(float)));
-      const int64_t want = h->private_rows < 0 ? (h->cfg.negative <= 5 ? std::min<int64_t>(10, slots) : 0)
+      const int64_t want = h->private_rows < 0 ? std::min<int64_t>(h->cfg.negative <= 5 ? 10 : kSnPrivRowsWide, slots)
                                                : h->private_rows;
       a.priv_n = h->sched == W2V_SCHED_PARALLEL ? (int32_t)std::min<int64_t>({slots, h->V, want}) : 0;
     }
