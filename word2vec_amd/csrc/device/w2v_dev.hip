@@ -187,6 +187,7 @@ struct w2v_dev {
   double kept_tokens = 0.0;         // expected kept centers of one epoch over the corpus (sum count * min(1, keep))
   std::vector<double> f, fk, node_f, node_fk;
   double path_len_f = 0.0, path_len_fk = 0.0;  // HS: mean Huffman code length over the tokens / the kept centers
+  int32_t replicas = 1;             // replicas of the exchange group this handle joined (w2v::set_replicas)
   int64_t last_wave_cap = 0;        // waves-in-flight cap of the last parallel launch (0: none; effective_max_waves)
   double hot_tau_rows = 0.0;        // automatic hot rows: expected concurrent updates threshold, W / C rows (0 = by vocab, hot_tau_for)
   double hot_tau_nodes = 1.0;       //   ... and Huffman nodes
@@ -203,6 +204,7 @@ struct w2v_dev {
 namespace w2v {
 int set_error(int code, const std::string& msg) { return fail(code, msg); }
 DevInfo dev_info(const w2v_dev* h) { return DevInfo{h->device, h->stream, h->V}; }
+void set_replicas(w2v_dev* h, int32_t n) { h->replicas = n < 1 ? 1 : n; }
 }  // namespace w2v
 
 // Per-word and per-node shares of the corpus (cached until the next upload).
@@ -1409,10 +1411,14 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     // the configuration without them +0.04..+0.34 / -0.71..+0.84) and run
     // 71.7 / 73.2 / 74.0 M words/s against 66.7 M (profiles/r05y_*, r05z_*,
     // r05aa_*). Above negative 5 the automatic setting keeps 4 private rows
-    // (the other slots stage atomic rows).
+    // (the other slots stage atomic rows) — for a handle that trains alone:
+    // two replicas summed by the exchange then lose -0.6 / -2.2 analogy on
+    // the 400 M-token replica gate (r05ab_tests.log, r05ad_tests.log; the
+    // rows' divisor assumes one replica's concurrency), so replicas keep none.
     {
       const int64_t slots = std::min<int64_t>(32, w2v::kSnPrivBytes / (h->pitch * (int64_t)sizeof(float)));
-      const int64_t want = h->private_rows < 0 ? std::min<int64_t>(h->cfg.negative <= 5 ? 10 : kSnPrivRowsWide, slots)
+      const int64_t wide = h->replicas > 1 ? 0 : kSnPrivRowsWide;
+      const int64_t want = h->private_rows < 0 ? std::min<int64_t>(h->cfg.negative <= 5 ? 10 : wide, slots)
                                                : h->private_rows;
       a.priv_n = h->sched == W2V_SCHED_PARALLEL ? (int32_t)std::min<int64_t>({slots, h->V, want}) : 0;
     }

@@ -22,6 +22,9 @@ struct DevInfo {
   int64_t V;
 };
 DevInfo dev_info(const w2v_dev* h);
+// The replicas of the exchange group a handle joined (w2v_group_create: all
+// ranks' members; 1 = none). The update policy reads it (launch_train).
+void set_replicas(w2v_dev* h, int32_t n);
 
 // Expected updates of each row of matrix k (0 = W, 1 = C, 2 = synapses1) per
 // corpus token, from the corpus statistics the handle holds (the rates the

@@ -549,6 +549,7 @@ int w2v_group_create(w2v_dev** members, int32_t n, const uint8_t* unique_id, int
       w2v_group_destroy(g);
       return fail_g(W2V_ERR_HIP, "w2v_group_create: synchronising the replicas failed");
     }
+  for (auto& x : g->m) w2v::set_replicas(x.h, nranks);
   *out = g;
   return W2V_OK;
 }
