@@ -439,8 +439,12 @@ def test_parallel_huge_window_reference_alpha_full_concurrency():
     a parallel launch caps its waves in flight by the vocabulary's pressure
     (effective_max_waves, w2v_dev.hip: here 9; every benchmarked shape stays
     uncapped) and trains this input to the sequential run's magnitude. An
-    explicit 512-wave launch still diverges, and fails LOUDLY
-    (W2V_ERR_DIVERGED), never with silent non-finite weights."""
+    explicit 512-wave launch fails LOUDLY (W2V_ERR_DIVERGED) when it diverges,
+    never with silent non-finite weights: with round 4's 64 private rows it
+    diverged in every suite run; the 96 rows skip-gram NS privatises since
+    round 5 damp more of this small vocabulary, and one suite
+    run in four then stayed finite (profiles/r05ag_tests.log), so that launch
+    may end either way, and a launch at alpha 5 must fail loudly."""
     for mode, wmax in (("cbow_ns", 10.0), ("sg_ns", 400.0)):
         o, d, order = _huge_window_trainer(mode, 2000, 0.025)
         st = d.train_epoch(0, order)
@@ -454,10 +458,19 @@ def test_parallel_huge_window_reference_alpha_full_concurrency():
         d.close()
     o, d, order = _huge_window_trainer("sg_ns", 2000, 0.025)
     d.set_max_waves(512)
+    try:
+        st = d.train_epoch(0, order)
+    except N.DevError as e:
+        assert e.code == N.W2V_ERR_DIVERGED
+    else:
+        W, Cm, _ = d.download_model()
+        assert st["nonfinite"] == 0 and np.isfinite(W).all() and np.isfinite(Cm).all()
+    assert d.policy()["wave_cap"] == 0  # the caller's cap, not the library's
+    d.close()
+    o, d, order = _huge_window_trainer("sg_ns", 2000, 5.0)
     with pytest.raises(N.DevError) as e:
         d.train_epoch(0, order)
     assert e.value.code == N.W2V_ERR_DIVERGED
-    assert d.policy()["wave_cap"] == 0  # the caller's cap, not the library's
     d.close()
 
 
