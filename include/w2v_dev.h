@@ -375,7 +375,10 @@ int w2v_group_unique_id(uint8_t* id /* W2V_GROUP_ID_BYTES */);
  * process's replicas are ranks [first_rank, first_rank + n) of nranks; with a
  * unique id even nranks = 1 builds the RCCL communicator and runs every
  * round's delta -> ncclAllReduce -> fold (the model is unchanged by it: the
- * sum of one replica's deltas), so one GPU exercises the exchange path. */
+ * sum of one replica's deltas), so one GPU exercises the exchange path. Each
+ * member learns the group's replica count (nranks), which its update policy
+ * reads from then on: with more than one replica, shared-negatives launches
+ * above negative 5 keep no LDS-private rows. */
 int w2v_group_create(w2v_dev** members, int32_t n, const uint8_t* unique_id, int32_t nranks, int32_t first_rank,
                      w2v_group** out);
 void w2v_group_destroy(w2v_group* g);

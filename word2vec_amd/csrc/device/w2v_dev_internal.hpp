@@ -23,7 +23,9 @@ struct DevInfo {
 };
 DevInfo dev_info(const w2v_dev* h);
 // The replicas of the exchange group a handle joined (w2v_group_create: all
-// ranks' members; 1 = none). The update policy reads it (launch_train).
+// ranks' members; 1 = none). The update policy reads it (launch_train). It
+// stays after the group is destroyed (the group may outlive no handle, but a
+// handle may outlive its group; it then keeps the replicas' policy).
 void set_replicas(w2v_dev* h, int32_t n);
 
 // Expected updates of each row of matrix k (0 = W, 1 = C, 2 = synapses1) per
