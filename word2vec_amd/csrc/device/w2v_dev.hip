@@ -83,6 +83,7 @@ struct Knobs {
   double priv_tail_avg = -1;     // W2V_PRIV_TAIL_AVG: private_average of the NS output rows past the 64th (0 = plain sum)
   int sn_per_cu = 0;             // W2V_SN_PER_CU: shared-negatives workgroups per CU (cap)
   double ctx_avg = -1;           // W2V_CTX_AVG: private_average of the CBOW context rows (0 = plain sum)
+  double priv_hs_tail_avg = -1;  // W2V_PRIV_HS_TAIL_AVG: private_average of the HS nodes past the 64th
   std::string desc;             // "NAME=value ..." of the variables that were set
 };
 
@@ -104,6 +105,7 @@ static Knobs read_knobs() {
   if (const char* v = get("W2V_PRIV_TAIL_AVG")) k.priv_tail_avg = std::max(0.0, std::atof(v));
   if (const char* v = get("W2V_SN_PER_CU")) k.sn_per_cu = std::max(0, std::atoi(v));
   if (const char* v = get("W2V_CTX_AVG")) k.ctx_avg = std::max(0.0, std::atof(v));
+  if (const char* v = get("W2V_PRIV_HS_TAIL_AVG")) k.priv_hs_tail_avg = std::max(0.0, std::atof(v));
   return k;
 }
 
@@ -988,7 +990,9 @@ static void priv_scales(w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool shared) {
       for (int p = 0; p < a.priv_n; ++p) {
         const int64_t j = a.priv_lo + p;
         const double m = !nodes ? 1.0 : cbow ? h->node_fk[(size_t)j] : win1 * h->node_f[(size_t)j];
-        a.priv_sc[p] = sc(m, a.flush_every, S);
+        // nodes past the 64th nearest the root: W2V_PRIV_HS_TAIL_AVG (experiments)
+        const double avg = p < 64 || h->knobs.priv_hs_tail_avg < 0.0 ? S : h->knobs.priv_hs_tail_avg;
+        a.priv_sc[p] = sc(m, a.flush_every, avg);
       }
     } else {
       for (int p = 0; p < a.priv_n; ++p) {
