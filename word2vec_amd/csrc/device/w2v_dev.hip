@@ -966,6 +966,16 @@ constexpr int64_t kWidePrivVocab = 500000;
 constexpr int64_t kSgNsPrivRows = 96;
 constexpr double kCtxAvgNs = 128.0;
 constexpr int64_t kSnPrivRowsWide = 4;  // shared negatives above negative 5 (launch_train)
+// CBOW-HS: 96 private Huffman nodes (64 context rows beside them) on
+// vocabularies >= 50 K. configs[1] (V 71 K, d200: 96 + 63 rows) 426 -> 468 M
+// words/s, its gate +15.9 / +5.9, text8-like CBOW-HS (V 98 K) +19.7..+22.1 /
+// +13.6..+14.3 (profiles/r05al_*). On the planted corpus's small tree the
+// extra nodes cost 6 similarity points at every flush average (8: -6, 4 / 2 /
+// 1: -8 / -14 / -18, 40 / 128: -13 / -18; r05al_4_*, r05am_*, r05an_*), so
+// small vocabularies keep 64; with fewer than 63 context rows beside them
+// (d300: 96 + 31) configs[1] gained 2 % and lost similarity (r05al_1_*, _2_*).
+constexpr int64_t kCbowHsPrivNodes = 96;
+constexpr int64_t kWideHsVocab = 50000;
 
 static void priv_scales(w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool shared) {
   for (int p = 0; p < w2v::kPrivMax; ++p) a.priv_sc[p] = 1.0f;
@@ -1344,8 +1354,12 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     // constantly, in a 70-100 K vocabulary rows 96..127 are evaluation words
     // (text8: "world", "city", "states", "war"). An explicit private_rows may
     // ask for up to kPrivMax.
+    // CBOW-HS on a vocabulary >= kWideHsVocab takes 96 nodes when the LDS
+    // still holds 64 context rows beside them (kCbowHsPrivNodes).
     const bool sg_ns = !h->cfg.cbow && !h->cfg.hs;
-    const int64_t auto_rows = !sg_ns ? 64 : h->V >= kWidePrivVocab ? w2v::kPrivMax : kSgNsPrivRows;
+    const bool wide_hs = h->cfg.cbow && h->cfg.hs && h->V >= kWideHsVocab && fit >= kCbowHsPrivNodes + w2v::kCtxMax - 1;
+    const int64_t auto_rows = !sg_ns ? (wide_hs ? kCbowHsPrivNodes : 64)
+                                     : h->V >= kWidePrivVocab ? w2v::kPrivMax : kSgNsPrivRows;
     int64_t P = std::min<int64_t>(fit, h->private_rows > 0 ? w2v::kPrivMax : auto_rows);
     if (h->private_rows >= 0) P = std::min<int64_t>(P, h->private_rows);
     const bool hs = h->cfg.hs != 0;
