@@ -14,6 +14,7 @@ parallel schedule and update policy are the only difference.
        (text8: 71.3 K, 254 K, 6 %)
   c1   configs[0]: SG-NS neg 5 d100 on the same text8-shaped corpus
   c2ns the reference's CBOW-NS mode (neg 5, d200) on configs[1]'s corpus
+  c1hs the reference's SG-HS mode (d100) on configs[0]'s corpus
 
 usage (repo root): python tests/golden/gen_headline_planted_golden.py c3 [seeds]
   -> tests/golden/quality_headline_<workload>_oracle.json (one record per seed).
@@ -37,6 +38,8 @@ WORKLOADS = {
     "c1": dict(corpus=TEXT8, mode="sg_ns", dim=100, negative=5, alpha=0.025),
     # the reference's CBOW-NS mode (no BASELINE config of its own) on configs[1]'s corpus and width
     "c2ns": dict(corpus=TEXT8, mode="cbow_ns", dim=200, negative=5, alpha=0.05),
+    # the reference's SG-HS mode on configs[0]'s corpus and width
+    "c1hs": dict(corpus=TEXT8, mode="sg_hs", dim=100, negative=0, alpha=0.025),
 }
 TRAIN = dict(window=5, iters=1, table_size=100_000_000, min_count=5, subsample=1e-4)
 SEEDS = (1, 2)
