@@ -270,10 +270,15 @@ HEADLINE_BOUNDS = {
     # +3.03..+3.49 / +3.00..+3.60, as with the atomic context rows of before
     # (+3.20..+3.72 / +3.15..+3.39): high = the largest + 2.
     "c2ns": {"analogy": (-1.0, 5.5), "similarity": (-1.0, 5.6)},
+    # the reference's SG-HS mode on configs[0]'s corpus (round 5: round 4's
+    # policy scored 24-27 analogy points BELOW the oracle here; 128 private
+    # nodes at 4 averaged contributions: +2.16..+3.17 / +0.03..+0.15 in three
+    # runs, profiles/r05au_*, r05av_*): high = the largest + 2; similarity +-1.
+    "c1hs": {"analogy": (-1.0, 5.2), "similarity": (-1.0, 1.0)},
 }
 
 
-@pytest.mark.parametrize("name", ["c3", "c2", "c1", "c2ns"])
+@pytest.mark.parametrize("name", ["c3", "c2", "c1", "c2ns", "c1hs"])
 def test_quality_headline_scale(name):
     import torch
 

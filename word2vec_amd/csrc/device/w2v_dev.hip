@@ -976,6 +976,18 @@ constexpr int64_t kSnPrivRowsWide = 4;  // shared negatives above negative 5 (la
 // (d300: 96 + 31) configs[1] gained 2 % and lost similarity (r05al_1_*, _2_*).
 constexpr int64_t kCbowHsPrivNodes = 96;
 constexpr int64_t kWideHsVocab = 50000;
+// Skip-gram HS: 128 private Huffman nodes (as many as fit: 127 at d300) at up
+// to 4 averaged contributions. With round 4's 64 nodes at 8 it scored 24-27
+// analogy points below the sequential oracle on configs[0]'s corpus (the
+// headline-scale SG-HS gate, new in round 5: every context of every center
+// walks the top of the tree, and nodes 64..127 as hot atomic rows were
+// Hogwild-stale); 64 nodes at 4 / 2 / 1: -21 / -17 / -13.5; 128 at 8: -4 and
+// one seed at -65; 128 at 4 / 2 / 1: +2.2..+3.2 / +7..+9 / +11; every variant
+// within a point on similarity (profiles/r05as_*, r05at_*, r05au_*, r05av_*).
+// The planted corpus: +4.5 / +1.4 against +3.1 / +0.7 before. Throughput on
+// configs[0]'s corpus 214 -> 309 M words/s, on configs[2]'s 44.0 -> 52.3 M
+// (0.71 -> 0.85 of 8 TB/s).
+constexpr double kSgHsNodeAverage = 4.0;
 
 static void priv_scales(w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool shared) {
   for (int p = 0; p < w2v::kPrivMax; ++p) a.priv_sc[p] = 1.0f;
@@ -1000,8 +1012,10 @@ static void priv_scales(w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool shared) {
       for (int p = 0; p < a.priv_n; ++p) {
         const int64_t j = a.priv_lo + p;
         const double m = !nodes ? 1.0 : cbow ? h->node_fk[(size_t)j] : win1 * h->node_f[(size_t)j];
-        // nodes past the 64th nearest the root: W2V_PRIV_HS_TAIL_AVG (experiments)
-        const double avg = p < 64 || h->knobs.priv_hs_tail_avg < 0.0 ? S : h->knobs.priv_hs_tail_avg;
+        // skip-gram HS caps the average at kSgHsNodeAverage; nodes past the
+        // 64th nearest the root: W2V_PRIV_HS_TAIL_AVG (experiments)
+        const double Sh = cbow ? S : std::min(S, kSgHsNodeAverage);
+        const double avg = p < 64 || h->knobs.priv_hs_tail_avg < 0.0 ? Sh : h->knobs.priv_hs_tail_avg;
         a.priv_sc[p] = sc(m, a.flush_every, avg);
       }
     } else {
@@ -1358,8 +1372,10 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     // still holds 64 context rows beside them (kCbowHsPrivNodes).
     const bool sg_ns = !h->cfg.cbow && !h->cfg.hs;
     const bool wide_hs = h->cfg.cbow && h->cfg.hs && h->V >= kWideHsVocab && fit >= kCbowHsPrivNodes + w2v::kCtxMax - 1;
-    const int64_t auto_rows = !sg_ns ? (wide_hs ? kCbowHsPrivNodes : 64)
-                                     : h->V >= kWidePrivVocab ? w2v::kPrivMax : kSgNsPrivRows;
+    const bool sg_hs = !h->cfg.cbow && h->cfg.hs;
+    const int64_t auto_rows = sg_hs ? w2v::kPrivMax
+                              : !sg_ns ? (wide_hs ? kCbowHsPrivNodes : 64)
+                                       : h->V >= kWidePrivVocab ? w2v::kPrivMax : kSgNsPrivRows;
     int64_t P = std::min<int64_t>(fit, h->private_rows > 0 ? w2v::kPrivMax : auto_rows);
     if (h->private_rows >= 0) P = std::min<int64_t>(P, h->private_rows);
     const bool hs = h->cfg.hs != 0;
