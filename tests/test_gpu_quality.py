@@ -106,9 +106,11 @@ def test_quality_paired_one_wave_within_1(name, mode):
 # one seed). Measured means: planted SG-NS +10.74 / +5.16, SG-HS +3.51 / +0.72,
 # CBOW-NS +9.39 / +0.29, CBOW-HS +17.75 / +2.00; text8-like SG-NS +27.74 /
 # +1.97, CBOW-HS +22.18 / +13.61; text8_small SG-NS +18.98 / +6.57, CBOW-HS
-# +24.90 / +19.32.
+# +24.90 / +19.32. Round 5: planted SG-HS with 128 private nodes at 4
+# averaged contributions +4.5 / +1.4 (probe) and +4.71 / +0.84
+# (r05aw_tests.log): its analogy high 5.6 -> 6.7.
 FULL_HIGH = {
-    ("planted", "sg_ns"): (12.8, 7.2), ("planted", "sg_hs"): (5.6, 2.8), ("planted", "cbow_ns"): (11.4, 2.3),
+    ("planted", "sg_ns"): (12.8, 7.2), ("planted", "sg_hs"): (6.7, 2.8), ("planted", "cbow_ns"): (11.4, 2.3),
     ("planted", "cbow_hs"): (19.8, 4.0), ("text8_like", "sg_ns"): (29.8, 4.0), ("text8_like", "cbow_hs"): (24.2, 15.7),
     ("text8_small", "sg_ns"): (22.0, 9.6), ("text8_small", "cbow_hs"): (27.9, 22.4),
 }

@@ -450,9 +450,12 @@ def test_shared_corpus_outlives_its_owner():
 # within [-6, +1] (measured -1.2 to -4.5 with one eight-replica run; the
 # sparse regime's -14 still fails it). 2.5 B tokens instead of configs[3]'s
 # 10 B keep the test near three minutes (10 B, one replica per run ~110 s:
-# HISTORY.md §6.2 has those runs).
+# HISTORY.md §6.2 has those runs). With both sides averaged over two runs the
+# similarity delta spread -4.43..+1.93 in seven suites (r05q ... r05aw_tests.log:
+# the single replica's own similarity moved 70.2-74.0), so its upper bound is
+# that largest + 1: +3.
 C3_SHAPE = dict(tokens=2_500_000_000, planted=0.05, planted_sents=0.02, seed=7)
-C3_BOUNDS = {"analogy": (-1.0, 35.0), "similarity": (-6.0, 1.0)}
+C3_BOUNDS = {"analogy": (-1.0, 35.0), "similarity": (-6.0, 3.0)}
 
 
 def test_configs3_shape_eight_replicas_hard_regime(tmp_path):
