@@ -976,6 +976,11 @@ constexpr int64_t kSnPrivRowsWide = 4;  // shared negatives above negative 5 (la
 // (d300: 96 + 31) configs[1] gained 2 % and lost similarity (r05al_1_*, _2_*).
 constexpr int64_t kCbowHsPrivNodes = 96;
 constexpr int64_t kWideHsVocab = 50000;
+// ... and nodes 64..95 flush at up to 4 averaged contributions: at the top
+// nodes' 8 the text8-like CBOW-HS gate had seeds at -5 / -8 / -9 similarity in
+// two suite runs of four (r05ax_tests.log, r05ay_1_*); at 4 / 2 six seed runs
+// each +10.8..+15.0 / +12.95..+13.7, configs[1] +16.6 / +6.5 (r05ay_*).
+constexpr double kCbowHsTailAverage = 4.0;
 // Skip-gram HS: 128 private Huffman nodes (as many as fit: 127 at d300) at up
 // to 4 averaged contributions. With round 4's 64 nodes at 8 it scored 24-27
 // analogy points below the sequential oracle on configs[0]'s corpus (the
@@ -1012,10 +1017,12 @@ static void priv_scales(w2v_dev* h, w2v::TrainArgs& a, int64_t G, bool shared) {
       for (int p = 0; p < a.priv_n; ++p) {
         const int64_t j = a.priv_lo + p;
         const double m = !nodes ? 1.0 : cbow ? h->node_fk[(size_t)j] : win1 * h->node_f[(size_t)j];
-        // skip-gram HS caps the average at kSgHsNodeAverage; nodes past the
-        // 64th nearest the root: W2V_PRIV_HS_TAIL_AVG (experiments)
+        // skip-gram HS caps the average at kSgHsNodeAverage, CBOW-HS its nodes
+        // past the 64th at kCbowHsTailAverage (W2V_PRIV_HS_TAIL_AVG: experiments)
         const double Sh = cbow ? S : std::min(S, kSgHsNodeAverage);
-        const double avg = p < 64 || h->knobs.priv_hs_tail_avg < 0.0 ? Sh : h->knobs.priv_hs_tail_avg;
+        const double tail = h->knobs.priv_hs_tail_avg >= 0.0 ? h->knobs.priv_hs_tail_avg
+                            : cbow ? std::min(S, kCbowHsTailAverage) : Sh;
+        const double avg = p < 64 ? Sh : tail;
         a.priv_sc[p] = sc(m, a.flush_every, avg);
       }
     } else {
