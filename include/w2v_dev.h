@@ -275,8 +275,9 @@ int w2v_dev_row_update_rates(w2v_dev* h, int32_t which, double* out, int64_t n);
  * many as fit the LDS budget, at most 64 for CBOW and HS, 96 for skip-gram NS,
  * 128 for skip-gram NS on a vocabulary >= 500 K words (rows past the 64th
  * flush with a gentler average), 96 Huffman nodes for CBOW-HS on a vocabulary
- * >= 50 K words when 63 context rows still fit, 128 nodes for skip-gram HS
- * (flushed at up to 4 averaged contributions)). n > 0 asks for up to 128;
+ * >= 50 K words when 63 context rows still fit (nodes 64..95 flushed at up to
+ * 4 averaged contributions), 128 nodes for skip-gram HS (all at up to 4);
+ * DESIGN.md §4.1). n > 0 asks for up to 128;
  * 0 disables them. Additive; no reference counterpart. */
 int w2v_dev_set_private_rows(w2v_dev* h, int32_t n);
 /* With private_rows = -1: privatise only the rows (Huffman nodes for HS, and
