@@ -40,6 +40,9 @@ WORKLOADS = {
     "c2ns": dict(corpus=TEXT8, mode="cbow_ns", dim=200, negative=5, alpha=0.05),
     # the reference's SG-HS mode on configs[0]'s corpus and width
     "c1hs": dict(corpus=TEXT8, mode="sg_hs", dim=100, negative=0, alpha=0.025),
+    # SG-HS at configs[2]'s corpus and width (probe golden; no test reads it)
+    "c3hs": dict(corpus=dict(n_tokens=50_000_000, filler=1_000_000, planted_frac=0.05), mode="sg_hs", dim=300,
+                 negative=0, alpha=0.025),
 }
 TRAIN = dict(window=5, iters=1, table_size=100_000_000, min_count=5, subsample=1e-4)
 SEEDS = (1, 2)

@@ -964,7 +964,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
 constexpr double kPrivTailAverage = 40.0;
 constexpr int64_t kWidePrivVocab = 500000;
 constexpr int64_t kSgNsPrivRows = 96;
-constexpr double kCtxAvgNs = 128.0;
+constexpr double kCtxAvgNs = 128.0;      // CBOW-NS context rows (launch_train has the measurements)
 constexpr int64_t kSnPrivRowsWide = 4;  // shared negatives above negative 5 (launch_train)
 // CBOW-HS: 96 private Huffman nodes (64 context rows beside them) on
 // vocabularies >= 50 K. configs[1] (V 71 K, d200: 96 + 63 rows) 426 -> 468 M
@@ -987,8 +987,8 @@ constexpr double kCbowHsTailAverage = 4.0;
 // headline-scale SG-HS gate, new in round 5: every context of every center
 // walks the top of the tree, and nodes 64..127 as hot atomic rows were
 // Hogwild-stale); 64 nodes at 4 / 2 / 1: -21 / -17 / -13.5; 128 at 8: -4 and
-// one seed at -65; 128 at 4 / 2 / 1: +2.2..+3.2 / +7..+9 / +11; every variant
-// within a point on similarity (profiles/r05as_*, r05at_*, r05au_*, r05av_*).
+// one seed at -65; 128 at 4 / 2 / 1: +2.2..+3.2 / +7..+9 / +11, each within a
+// point on similarity (profiles/r05as_*, r05at_*, r05au_*, r05av_*).
 // The planted corpus: +4.5 / +1.4 against +3.1 / +0.7 before. Throughput on
 // configs[0]'s corpus 214 -> 309 M words/s, on configs[2]'s 44.0 -> 52.3 M
 // (0.71 -> 0.85 of 8 TB/s).
