@@ -43,6 +43,9 @@ WORKLOADS = {
     # SG-HS at configs[2]'s corpus and width (probe golden; no test reads it)
     "c3hs": dict(corpus=dict(n_tokens=50_000_000, filler=1_000_000, planted_frac=0.05), mode="sg_hs", dim=300,
                  negative=0, alpha=0.025),
+    # CBOW-HS at configs[2]'s corpus and width (probe golden; no test reads it)
+    "c3cbhs": dict(corpus=dict(n_tokens=50_000_000, filler=1_000_000, planted_frac=0.05), mode="cbow_hs", dim=300,
+                   negative=0, alpha=0.05),
 }
 TRAIN = dict(window=5, iters=1, table_size=100_000_000, min_count=5, subsample=1e-4)
 SEEDS = (1, 2)
