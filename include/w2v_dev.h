@@ -296,6 +296,14 @@ int w2v_dev_private_rate_used(w2v_dev* h, float* mu);
  * window 150 / negative 80 diverges from 128 waves up, as the reference's own
  * OpenMP loop does on 8 threads). Every benchmarked shape stays uncapped. */
 int w2v_dev_wave_cap_used(w2v_dev* h, int64_t* waves);
+/* The replica count the update policy assumes (no reference counterpart: the
+ * reference trains one model). w2v_group_create sets it to the group's ranks;
+ * the one-GPU rehearsal of an N-rank run (each rank a one-rank group, the
+ * ranks combined over gloo) sets it to N, so its launches use the policy an
+ * N-GPU run uses (shared negatives: no private C rows in a replica group).
+ * n >= 1. */
+int w2v_dev_set_replica_count(w2v_dev* h, int32_t n);
+int w2v_dev_replica_count(w2v_dev* h, int32_t* n);
 /* flush_centers: workgroup centers between flushes (0 = auto: 1024 for NS, 64
  * for HS); average_over: the concurrency a private row's summed deltas are
  * scaled down to (default 8; 0 = plain sum). */

@@ -54,6 +54,7 @@ _SIG = {
     "orc_stream": (None, [_P, _P, _P, _P]),
     "orc_train_replay": (None, [_P, _I32, _P, _P, _P, _I64]),
     "orc_train_philox": (None, [_P, _I32, _I32, _P, _U64, _I64]),
+    "orc_train_philox_omp": (None, [_P, _I32, _I32, _I32, _P, _U64, _I64]),
     "orc_philox": (None, [_P, _U64, _P]),
     "orc_set_shared_negatives": (None, [_P, _I32]),
     "orc_train_omp": (_I64, [_P, _I32, _I64, _U32]),
@@ -250,6 +251,13 @@ class Oracle:
     def train_philox(self, epoch0, epochs, orders, key, cw0=0):
         orders = np.ascontiguousarray(orders, np.int64)
         self.L.orc_train_philox(self.h, epoch0, epochs, _p(orders), key, cw0)
+
+    def train_philox_omp(self, threads, epoch0, epochs, orders, key, cw0=0):
+        """The reference's OpenMP loop (Word2Vec.cpp:375-394, static schedule,
+        Hogwild updates) on `threads` threads with the Philox draws: differs
+        from train_philox only by the threads' concurrency."""
+        orders = np.ascontiguousarray(orders, np.int64)
+        self.L.orc_train_philox_omp(self.h, threads, epoch0, epochs, _p(orders), key, cw0)
 
     def set_shared_negatives(self, on: bool = True):
         """Shared-negatives minibatch skip-gram (configs[4]) for later training calls."""

@@ -713,6 +713,62 @@ void orc_train_philox(void* h, int32_t epoch0, int32_t epochs, const int64_t* or
   }
 }
 
+// The reference's OpenMP epoch (Word2Vec.cpp:375-394) on `threads` threads
+// over a given order, with the Philox draws: `#pragma omp parallel for` with
+// the default (static) schedule, so thread t walks the t-th contiguous block
+// of the order; alpha refreshed every 10th index from the shared word counter
+// (:379-380) and the counter bumped atomically (:392-393); the matrices are
+// updated without synchronisation (the reference's Hogwild). The Philox draws
+// are keyed by (epoch, sentence, position), so this differs from
+// orc_train_philox ONLY by the threads' concurrency: the anchor of what the
+// reference's own parallel loop does to the vectors.
+void orc_train_philox_omp(void* h, int32_t threads, int32_t epoch0, int32_t epochs, const int64_t* orders,
+                          uint64_t key, int64_t cw0) {
+  Orc& m = *H(h);
+  const int64_t n = (int64_t)m.off.size() - 1;
+  int64_t cw = cw0;
+  float alpha = m.cfg.init_alpha;
+#ifdef _OPENMP
+  omp_set_num_threads(threads);
+#else
+  (void)threads;
+#endif
+  for (int e = 0; e < epochs; ++e) {
+    const int64_t* order = orders + (int64_t)e * n;
+#pragma omp parallel
+    {
+      PhiloxDraws dr;
+      dr.k0 = (uint32_t)key; dr.k1 = (uint32_t)(key >> 32);
+      dr.window = m.cfg.window; dr.table_size = m.cfg.table_size;
+      dr.epoch = (uint32_t)(epoch0 + e);
+#pragma omp for schedule(static)
+      for (int64_t i = 0; i < n; ++i) {
+        if (i % 10 == 0) {
+          int64_t snap;
+#pragma omp atomic read
+          snap = cw;
+          float a = schedule(m, snap);
+#pragma omp atomic write
+          alpha = a;
+        }
+        float a_now;
+#pragma omp atomic read
+        a_now = alpha;
+        const int64_t s = order[i];
+        const int32_t* sent = m.ids.data() + m.off[s];
+        const int len = (int)(m.off[s + 1] - m.off[s]);
+        if (m.shared_negatives) sgsn_sentence(m, sent, len, a_now, dr, s);
+        else if (m.cfg.cbow) cbow_sentence(m, sent, len, a_now, dr, s);
+        else sg_sentence(m, sent, len, a_now, dr, s);
+#pragma omp atomic
+        cw += len;
+      }
+    }
+  }
+  m.current_words = cw;
+  m.last_alpha = alpha;
+}
+
 // Shared-negatives minibatch skip-gram (sgsn_sentence) for every later training call.
 void orc_set_shared_negatives(void* h, int32_t on) { H(h)->shared_negatives = on != 0; }
 

@@ -83,6 +83,8 @@ def headline(name, variants):
             E = Cm if G.eval_matrix(name) == 1 else W
             got.append(scores(words, E, qs, prs, torch.device("cuda", 0)) if st["nonfinite"] == 0 else (np.nan, np.nan))
             ref.append([r["analogy"], r["similarity"]])
+            print(f"  {nm} seed {r['seed']}: {np.round(np.array(got[-1]) - ref[-1], 2).tolist()} "
+                  f"({time.time() - t0:.0f} s)", file=sys.stderr, flush=True)
         report(name, nm, spec, got, ref, pol, t0)
 
 

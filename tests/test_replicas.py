@@ -194,6 +194,10 @@ class StubGroupLib:
     def w2v_group_destroy(self, g):
         self.calls.append(("destroy", g.value))
 
+    def w2v_dev_set_replica_count(self, h, n):
+        self.calls.append(("replica_count", h, n))
+        return 0
+
     def w2v_dev_last_error(self):
         return b"stub"
 
@@ -262,6 +266,11 @@ def test_make_averager_stub_group_world2(share):
         _, hs, uid, nranks, first = creates[0]
         assert hs == [0x1000 + rank] and uid == uid0
         assert (nranks, first) == ((1, 0) if share else (world, rank))
+        # the rehearsal's policy assumes the run's replica count, not its one-rank group's
+        rc = [c for c in calls if c[0] == "replica_count"]
+        assert rc == ([("replica_count", 0x1000 + rank, world)] if share else [])
+        if share:
+            assert calls.index(rc[0]) > calls.index(creates[0])
         # only rank 0 makes ids: one per rank in the rehearsal, one for the group otherwise
         n_ids = sum(c[0] == "unique_id" for c in calls)
         assert n_ids == ((world if share else 1) if rank == 0 else 0)

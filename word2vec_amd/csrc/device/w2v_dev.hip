@@ -84,6 +84,7 @@ struct Knobs {
   int sn_per_cu = 0;             // W2V_SN_PER_CU: shared-negatives workgroups per CU (cap)
   double ctx_avg = -1;           // W2V_CTX_AVG: private_average of the CBOW context rows (0 = plain sum)
   double priv_hs_tail_avg = -1;  // W2V_PRIV_HS_TAIL_AVG: private_average of the HS nodes past the 64th
+  double hs_hot_avg = -1;        // W2V_HS_HOT_AVG: concurrent updates the atomic hot HS nodes' deltas are scaled to (0 = none)
   std::string desc;             // "NAME=value ..." of the variables that were set
 };
 
@@ -106,6 +107,7 @@ static Knobs read_knobs() {
   if (const char* v = get("W2V_SN_PER_CU")) k.sn_per_cu = std::max(0, std::atoi(v));
   if (const char* v = get("W2V_CTX_AVG")) k.ctx_avg = std::max(0.0, std::atof(v));
   if (const char* v = get("W2V_PRIV_HS_TAIL_AVG")) k.priv_hs_tail_avg = std::max(0.0, std::atof(v));
+  if (const char* v = get("W2V_HS_HOT_AVG")) k.hs_hot_avg = std::max(0.0, std::atof(v));
   return k;
 }
 
@@ -201,6 +203,11 @@ struct w2v_dev {
   double last_private_rate = 0.0;
   int32_t last_priv = 0, last_ctx = 0;
   int32_t last_flush = 0, last_ctx_flush = 0;
+  double last_hs_hot_avg = 0.0;     // the hot-node average of the last launch (0: none)
+  // per atomic hot Huffman node [hot_s, V - 1): the scale of its deltas (hot_node_scales)
+  std::vector<float> hot_sc_h;
+  float* hot_sc_d = nullptr;
+  int64_t hot_sc_cap = 0;
 };
 
 namespace w2v {
@@ -461,7 +468,7 @@ void w2v_dev_destroy(w2v_dev* h) {
   dfree(h->keep); dfree(h->table); dfree(h->codes); dfree(h->points); dfree(h->coff);
   release_corpus(h); dfree(h->replay); dfree(h->replay_off);
   dfree(h->counters); dfree(h->work);
-  dfree(h->scratch_f); dfree(h->scratch_codes); dfree(h->xfer_f); dfree(h->wide_scratch);
+  dfree(h->scratch_f); dfree(h->scratch_codes); dfree(h->xfer_f); dfree(h->wide_scratch); dfree(h->hot_sc_d);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -1131,6 +1138,11 @@ static int64_t effective_max_waves(w2v_dev* h, int64_t count) {
   const double cap = std::floor(kPairPressure * (double)h->V / T);
   const int64_t per_simd = h->nv <= 2 ? 8 : 4;  // kMinWaves<NV>
   const int64_t chip = (int64_t)h->n_cu * 4 * per_simd;
+  // The waves the launch would run: min(chip, count) with count in sentences
+  // is exact also when launch_train cuts sentences into segments (nseg > 1),
+  // because it does so only when the sentences alone fill the grid (count >=
+  // the grid's waves), and then min(chip, count x nseg) = chip = min(chip,
+  // count).
   return cap < (double)std::min(chip, count) ? std::max<int64_t>(1, (int64_t)cap) : 0;
 }
 
@@ -1273,6 +1285,44 @@ static int32_t auto_hs_flush(w2v_dev* h, int64_t count, int64_t G) {
   int32_t fe = 64;
   while (fe < kHsFlushMax && 2.0 * fe * kHsFlushes <= cpw) fe *= 2;
   return fe;
+}
+
+// Atomic hot Huffman nodes (hot_s .. V - 2 below the LDS-private ones): each
+// of their updates is a memory-side add computed from the node as the wave
+// read it, while `waves` x m(node) other updates of the node are in flight
+// (m = its expected updates per kept center: skip-gram (window + 1) x the
+// token share below it, CBOW the kept-center share). With W2V_HS_HOT_AVG = S
+// their deltas are scaled by 1 / max(1, waves m / S): at most S concurrent
+// stale contributions, the damping the private nodes' averaged flush gives
+// the nodes above them.
+static int hot_node_scales(w2v_dev* h, w2v::TrainArgs& a, double waves, int64_t nodes) {
+  const double S = h->knobs.hs_hot_avg >= 0.0 ? h->knobs.hs_hot_avg : 0.0;
+  h->last_hs_hot_avg = 0.0;
+  if (!h->cfg.hs || h->sched != W2V_SCHED_PARALLEL || !(S > 0.0) || nodes <= 0) return W2V_OK;
+  row_stats(h);
+  if (!h->stats_ok || (int64_t)h->node_f.size() != h->V - 1) return W2V_OK;
+  const bool cbow = h->cfg.cbow != 0;
+  const double win1 = (double)h->cfg.window + 1.0;
+  std::vector<float> sc((size_t)nodes);
+  for (int64_t k = 0; k < nodes; ++k) {
+    const int64_t j = a.hot_s + k;
+    const double m = cbow ? h->node_fk[(size_t)j] : win1 * h->node_f[(size_t)j];
+    sc[(size_t)k] = (float)(1.0 / std::max(1.0, waves * m / S));
+  }
+  if (sc != h->hot_sc_h || !h->hot_sc_d) {
+    HIP_TRY(hipStreamSynchronize(h->stream));  // an earlier launch may still read the old scales
+    if (nodes > h->hot_sc_cap) {
+      dfree(h->hot_sc_d);
+      h->hot_sc_cap = 0;
+      HIP_TRY(hipMalloc(&h->hot_sc_d, (size_t)nodes * sizeof(float)));
+      h->hot_sc_cap = nodes;
+    }
+    HIP_TRY(hipMemcpy(h->hot_sc_d, sc.data(), (size_t)nodes * sizeof(float), hipMemcpyHostToDevice));
+    h->hot_sc_h.swap(sc);
+  }
+  a.hot_sc = h->hot_sc_d;
+  h->last_hs_hot_avg = S;
+  return W2V_OK;
 }
 
 static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int64_t count) {
@@ -1540,6 +1590,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     grid = dim3((unsigned)g);
     block = dim3(threads);
   }
+  a.hot_sc = nullptr;
   {
     // The rule counts every wave the chip could run, not this launch's grid:
     // a small launch (a round's slice, a wave cap) still spreads over the XCDs,
@@ -1553,6 +1604,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     h->last_hot_nodes = h->cfg.hs ? hot.second : 0;
     h->last_priv = a.priv_n;
     h->last_ctx = a.ctx_n;
+    if (int rc = hot_node_scales(h, a, (double)resident_waves, hot.second)) return rc;
   }
   // Sentence segments as work items (parallel Philox schedule): the launch's
   // last round shrinks from a whole sentence per wave to one segment. With
@@ -1776,6 +1828,19 @@ int w2v_dev_private_rate_used(w2v_dev* h, float* mu) {
 int w2v_dev_wave_cap_used(w2v_dev* h, int64_t* waves) {
   if (!h) return fail(W2V_ERR_ARG, "null handle");
   if (waves) *waves = h->last_wave_cap;
+  return W2V_OK;
+}
+
+int w2v_dev_set_replica_count(w2v_dev* h, int32_t n) {
+  if (!h) return fail(W2V_ERR_ARG, "null handle");
+  if (n < 1) return fail(W2V_ERR_ARG, "replica count must be >= 1");
+  w2v::set_replicas(h, n);
+  return W2V_OK;
+}
+
+int w2v_dev_replica_count(w2v_dev* h, int32_t* n) {
+  if (!h || !n) return fail(W2V_ERR_ARG, "null argument");
+  *n = h->replicas;
   return W2V_OK;
 }
 

@@ -108,6 +108,7 @@ struct TrainArgs {
   // (64-bit bounds moved every hot / private test onto the VALU).
   int32_t hot_wc;              // W / C rows [0, hot_wc) update with atomics (shared-negatives: sc1 traffic)
   int32_t hot_s;               // synapses1 rows [hot_s, V-1) update with atomics
+  const float* hot_sc;         // per hot node j >= hot_s: its deltas' scale, hot_sc[j - hot_s] (null: 1; hot_node_scales)
   int32_t strict;              // 1: drain own atomics before re-reading (sequential schedule)
   const float* priv_M;         // output matrix whose hottest rows are privatised in LDS (or null)
   int32_t priv_lo;             // privatised rows [priv_lo, priv_lo + priv_n)
@@ -823,6 +824,11 @@ __device__ __forceinline__ void hs_apply(const TrainArgs& a, int T, int row_l, i
       if (pr.has(row)) {
         priv_add<NV>(pr, row, a.dim, lane, delta);
       } else if (row >= a.hot_s) {
+        if (a.hot_sc) {  // damped to the hot-node average (wave-uniform row: one scalar load)
+          const float s = a.hot_sc[row - a.hot_s];
+#pragma unroll
+          for (int v = 0; v < NV; ++v) delta[v] *= s;
+        }
         if (!(W2V_EXP_SKIP & 1)) atomic_add_row<NV>(a.S, row, a.pitch, a.dim, lane, delta);
       } else {
 #pragma unroll

@@ -106,6 +106,10 @@ class TorchAverager:
         pass
 
 
+def _handle(trainer):
+    return trainer.h.value if isinstance(trainer.h, C.c_void_p) else trainer.h
+
+
 class NativeAverager:
     """The C-ABI's RCCL replica group (w2v_group_*) over this process's device
     handles; `unique_id` (W2V_GROUP_ID_BYTES bytes from group_unique_id() on
@@ -244,6 +248,10 @@ def make_averager(trainer, mats, world: int, rank: int, mode: str, overlap: bool
     uids = [[group_unique_id() for _ in range(world)] if rank == 0 else None]
     dist.broadcast_object_list(uids, src=0)
     native = NativeAverager([trainer], uids[0][rank], 1, 0, overlap=overlap, mode=mode)
+    # the one-rank group told the handle "1 replica": the rehearsal trains with
+    # the policy an N-GPU run uses
+    native.N.check(native.lib, native.lib.w2v_dev_set_replica_count(_handle(trainer), int(world)),
+                   "w2v_dev_set_replica_count")
     return RehearsalAverager(native, TorchAverager(mats, world)), "rehearsal: one-rank w2v_group per process + gloo mean"
 
 
