@@ -219,6 +219,12 @@ class Word2Vec {
   // Wall seconds of each epoch of the last train call (the device epoch,
   // w2v_dev_train_epoch / the replicas' rounds; no host setup or transfers).
   std::vector<double> epoch_seconds;
+  // Data-parallel replicas (gpu_devices) of the last train call: the
+  // exchanges run (w2v_group_info rounds) and how far the replicas' models
+  // were apart after the last one: max over replicas and matrices of
+  // max |M_i - M_0| / max |M_0| (w2v_dev_model_max_diff; -1 = not measured).
+  int64_t replica_rounds = 0;
+  double replica_max_diff = -1.0;
   // Last device error (empty if none).
   std::string last_error;
 

@@ -142,6 +142,13 @@ int w2v_dev_upload_table(w2v_dev* h, const uint32_t* table, int64_t n);
  * W and C have V rows, synapses1 V-1. NULL skips a matrix. */
 int w2v_dev_upload_model(w2v_dev* h, const float* W, const float* C, const float* syn1);
 int w2v_dev_download_model(w2v_dev* h, float* W, float* C, float* syn1);
+/* How far two handles' resident models are apart: out[k] = max |A_k - B_k|
+ * and out[3 + k] = max |A_k| for k = W, C, synapses1 (0 for an absent one; a
+ * NaN in either counts as infinitely apart). The handles may sit on
+ * different devices (b's matrix is staged on a's). No reference counterpart:
+ * it checks that the replicas of a group hold one model, up to the fp32
+ * rounding of their folds, after the last exchange. */
+int w2v_dev_model_max_diff(w2v_dev* a, w2v_dev* b, float out[6]);
 /* Row-sparse transfers: rows[k] of matrix `which` (0 = W, 1 = C, 2 =
  * synapses1) <-> data[k * word_dim .. +word_dim) (host, dense). The per-call
  * methods (Word2Vec::train_sentence_*, Word2Vec.h:83-84) move only the rows a

@@ -94,6 +94,9 @@ int64_t w2v_model_epochs_done(w2v_model* m);
 /* Word2Vec::epoch_seconds[i] of the last train call (-1 when i is out of range). */
 double w2v_model_epoch_seconds(w2v_model* m, int64_t i);
 int64_t w2v_model_current_words(w2v_model* m);
+/* Word2Vec::replica_rounds / replica_max_diff of the last train call. */
+int64_t w2v_model_replica_rounds(w2v_model* m);
+double w2v_model_replica_max_diff(w2v_model* m);
 int w2v_model_read_vocab(w2v_model* m, const char* path);
 /* Word2Vec::create_huffman_tree / make_table / precalc_sampling
  * (Word2Vec.h:70-72; Word2Vec.cpp:32-130): the vocabulary products

@@ -444,7 +444,12 @@ def test_parallel_huge_window_reference_alpha_full_concurrency():
     diverged in every suite run; the 96 rows skip-gram NS privatises since
     round 5 damp more of this small vocabulary, and one suite
     run in four then stayed finite (profiles/r05ag_tests.log), so that launch
-    may end either way, and a launch at alpha 5 must fail loudly."""
+    may end either way — but which way is checked: a divergence must come
+    with the device's non-finite counter set, and a finite end must be the
+    Hogwild inflation the cap exists for (max |W| above the capped run's, as
+    at 16 waves: 667 against ~140-290). A launch at alpha 5 must fail
+    loudly."""
+    capped_max = None
     for mode, wmax in (("cbow_ns", 10.0), ("sg_ns", 400.0)):
         o, d, order = _huge_window_trainer(mode, 2000, 0.025)
         st = d.train_epoch(0, order)
@@ -455,6 +460,8 @@ def test_parallel_huge_window_reference_alpha_full_concurrency():
         assert np.isfinite(W).all() and np.isfinite(Cm).all() and np.abs(W).max() < wmax
         # skip-gram: ~12 K rows per center, capped; CBOW-NS: 232, below its 200 sentences' waves
         assert (0 < pol["wave_cap"] <= 16) if mode == "sg_ns" else pol["wave_cap"] == 0
+        if mode == "sg_ns":
+            capped_max = float(np.abs(W).max())
         d.close()
     o, d, order = _huge_window_trainer("sg_ns", 2000, 0.025)
     d.set_max_waves(512)
@@ -462,9 +469,13 @@ def test_parallel_huge_window_reference_alpha_full_concurrency():
         st = d.train_epoch(0, order)
     except N.DevError as e:
         assert e.code == N.W2V_ERR_DIVERGED
+        assert d.read_stats()["nonfinite"] > 0  # the counter that raised it
+        print("huge window sg_ns at 512 waves: diverged (W2V_ERR_DIVERGED)")
     else:
         W, Cm, _ = d.download_model()
         assert st["nonfinite"] == 0 and np.isfinite(W).all() and np.isfinite(Cm).all()
+        print(f"huge window sg_ns at 512 waves: finite, max |W| {np.abs(W).max():.3g} (capped {capped_max:.3g})")
+        assert np.abs(W).max() > capped_max  # without the cap the weights inflate
     assert d.policy()["wave_cap"] == 0  # the caller's cap, not the library's
     d.close()
     o, d, order = _huge_window_trainer("sg_ns", 2000, 5.0)

@@ -240,47 +240,59 @@ def test_quality_shared_negatives_c5_hyperparameters():
 # The planted-relation corpus of tests/planted_ids.py sized like the bench
 # presets (configs[2]: 50 M tokens, V 717 K, SG-NS d300; configs[1] / [0]: a
 # text8-shaped 17 M-token corpus, V 71 K, CBOW-HS d200 / SG-NS d100), paired
-# with the sequential oracle (tests/golden/gen_headline_planted_golden.py:
-# same initial weights, Philox key and sentence order), trained by the GPU in
-# the shipped throughput configuration (Philox, parallel schedule, the
-# library's automatic update policy for that vocabulary: hot-row threshold,
-# LDS-private rows, segments). Bounds on the mean paired delta over the
-# golden's seeds, (low, high) per metric. Low is north_star's -1 point
-# everywhere. High is +1 (two-sided) where the GPU lands within a point of the
-# reference, else the measured delta + 1 (a bound with no upper
-# end passes a change that inflates scores by any amount): where the parallel
-# update policy scores ABOVE the sequential reference — measured (round 4,
-# r04a / r04b / r04n, 2 seeds): configs[2] analogy +1.80 to
-# +2.32 per seed (mean +1.97 / +2.06: the damped, aggregated updates of the
-# frequent rows), configs[1] CBOW-HS +13.66 / +6.34 (per seed +13.40..+13.91 /
-# +6.02..+6.67), configs[0] similarity +3.28 / +3.29 — the high bound is that
-# mean + 1. A policy change that moves a score past it fails here and is
-# explained in DESIGN.md §2 before the bound moves. Moved once, round 5:
-# configs[1]'s HS flush interval went from 256 / 128 to 512 / 256 centers
-# (auto_hs_flush, w2v_dev.hip: 331 -> 420-428 M words/s) and its analogy
-# from +13.1..+13.7 (five leases) to +16.4 / +17.3 (profiles/r05j_2_*,
-# r05k_tests.log; similarity unchanged at +6.3 / +6.45): analogy high 18.4.
-# With that policy unchanged, four whole-suite runs then spread +14.0..+17.8 /
-# +4.3..+6.47 (r05k, r05n, r05o, r05s_tests.log): high = the largest + 2 /
-# + 1.5, so the run-to-run spread of one policy does not decide the gate.
-HEADLINE_BOUNDS = {
-    "c3": {"analogy": (-1.0, 3.1), "similarity": (-1.0, 1.0)},
-    "c2": {"analogy": (-1.0, 19.8), "similarity": (-1.0, 8.0)},
-    "c1": {"analogy": (-1.0, 1.0), "similarity": (-1.0, 4.3)},
-    # the reference's CBOW-NS mode on configs[1]'s corpus (round 5: its hottest
-    # context rows LDS-private). Measured (r05w, three runs):
-    # +3.03..+3.49 / +3.00..+3.60, as with the atomic context rows of before
-    # (+3.20..+3.72 / +3.15..+3.39): high = the largest + 2.
-    "c2ns": {"analogy": (-1.0, 5.5), "similarity": (-1.0, 5.6)},
-    # the reference's SG-HS mode on configs[0]'s corpus (round 5: round 4's
-    # policy scored 24-27 analogy points BELOW the oracle here; 128 private
-    # nodes at 4 averaged contributions: +2.16..+3.17 / +0.03..+0.15 in three
-    # runs, profiles/r05au_*, r05av_*): high = the largest + 2; similarity +-1.
-    "c1hs": {"analogy": (-1.0, 5.2), "similarity": (-1.0, 1.0)},
+# with the reference (tests/golden/gen_headline_planted_golden.py: same
+# initial weights, Philox draws and sentence order), trained by the GPU in the
+# shipped throughput configuration (Philox, parallel schedule, the library's
+# automatic update policy for that vocabulary).
+#
+# THE REFERENCE, two ways (VERDICT r05 "next" 2): its sequential loop
+# (quality_headline_<w>_oracle.json) and its OpenMP Hogwild loop on 16
+# threads as the reference build runs it (Word2Vec.cpp:375-394,
+# quality_headline_<w>_omp16_oracle.json, two runs per seed: the loop is not
+# deterministic). Measured OMP16 - sequential (analogy / similarity): c1 +0.06
+# / +0.93, c1hs -0.05 / -0.08, c2 +4.63 / -3.37, c2ns +0.38 / +1.72, c3 +1.96
+# / +0.34, c3hs and c3cbhs in DESIGN.md §2: the reference's own threads move
+# CBOW-HS by ~4 points. A result of the reference is anything in the band
+# [min(seq, omp16), max(seq, omp16)] per metric; north_star's +-1 is that band
+# widened by a point each way. Every gate asserts the LOW end (not more than a
+# point below both reference runs). The HIGH end is the band's + 1 except
+# where the throughput policy is a documented deviation ABOVE the reference
+# (DEVIATION_HIGH: its damped, aggregated updates of the frequent rows score
+# higher than per-update Hogwild), whose highs are frozen at the
+# round-5 values against the sequential run (a bound is not moved
+# to follow a result).
+DEVIATION_HIGH = {
+    "c2": {"analogy": 19.8, "similarity": 8.0},
+    "c1": {"similarity": 4.3},
+    "c2ns": {"analogy": 5.5, "similarity": 5.6},
+    "c1hs": {"analogy": 5.2},
 }
+# GPU runs per golden seed (the parallel schedule is not deterministic): the
+# large-vocabulary CBOW-HS per-run spread is ~2 analogy points (profiles/r06c_*,
+# r06d_*), so its gate averages two (skip-gram HS, 15 s per run at its 256
+# waves, keeps one: its band is 1.3 points wide, r06_omp16_c3hs.log).
+HEADLINE_RUNS = {"c3cbhs": 2}
+HEADLINE_WORKLOADS = ["c3", "c2", "c1", "c2ns", "c1hs", "c3hs", "c3cbhs"]
 
 
-@pytest.mark.parametrize("name", ["c3", "c2", "c1", "c2ns", "c1hs"])
+def reference_band(name):
+    """{metric: (lo, hi)}: the sequential and the OMP16 golden means (the band
+    collapses to the sequential mean when no OMP16 golden exists)."""
+    from tests.golden import gen_headline_planted_golden as G
+
+    seq = json.loads(G.golden_path(name).read_text())
+    refs = [np.array([[r["analogy"], r["similarity"]] for r in seq["scores"]]).mean(0)]
+    p = G.golden_path(name, 16)
+    if p.exists():
+        omp = json.loads(p.read_text())
+        assert omp["train"] == seq["train"] and omp["corpus"] == seq["corpus"]
+        assert [r["seed"] for r in omp["scores"]] == [r["seed"] for r in seq["scores"]]
+        refs.append(np.array([[r["analogy"], r["similarity"]] for r in omp["scores"]]).mean(0))
+    refs = np.array(refs)
+    return {m: (float(refs[:, k].min()), float(refs[:, k].max())) for k, m in enumerate(("analogy", "similarity"))}, refs
+
+
+@pytest.mark.parametrize("name", HEADLINE_WORKLOADS)
 def test_quality_headline_scale(name):
     import torch
 
@@ -290,26 +302,35 @@ def test_quality_headline_scale(name):
     gold = json.loads(G.golden_path(name).read_text())
     w = G.WORKLOADS[name]
     assert gold["corpus"] == w["corpus"] and gold["train"] == G.TRAIN and gold["mode"] == w["mode"]
+    band, refs = reference_band(name)
     ids, soff, counts, words, raw, qs, prs = G.corpus(name)
-    got, ref = [], []
+    got = []
     for r in gold["scores"]:
         assert r["V"] == counts.size and r["raw_tokens"] == raw
-        W0, C0, S0, key = G.init(name, r["seed"], counts.size)
-        t = gpu_trainer(counts, ids, soff, raw, w["mode"], w["dim"], w["negative"], w["alpha"], W0, C0, S0, key,
-                        window=G.TRAIN["window"], subsample=G.TRAIN["subsample"], table_size=G.TRAIN["table_size"])
-        del W0, C0, S0
-        t.train_epoch(0, G.order_of(r["seed"], soff.size - 1))
-        pol = t.policy()
-        W, Cm, _ = t.download_model()
-        t.close()
-        E = Cm if G.eval_matrix(name) == 1 else W
-        got.append(scores(words, E, qs, prs, torch.device("cuda", 0)))
-        ref.append([r["analogy"], r["similarity"]])
-        del W, Cm, E
-    got, ref = np.array(got), np.array(ref)
-    dl = (got - ref).mean(0)
-    print(f"headline-scale {name} ({w['mode']} d{w['dim']}, V {counts.size}, {raw} tokens): gpu {got.mean(0).round(2)} "
-          f"oracle {ref.mean(0).round(2)} delta {dl.round(2)} per seed {(got - ref).round(2).tolist()} policy {pol}")
+        runs = []
+        for _ in range(HEADLINE_RUNS.get(name, 1)):
+            W0, C0, S0, key = G.init(name, r["seed"], counts.size)
+            t = gpu_trainer(counts, ids, soff, raw, w["mode"], w["dim"], w["negative"], w["alpha"], W0, C0, S0, key,
+                            window=G.TRAIN["window"], subsample=G.TRAIN["subsample"],
+                            table_size=G.TRAIN["table_size"])
+            del W0, C0, S0
+            t.train_epoch(0, G.order_of(r["seed"], soff.size - 1))
+            pol = t.policy()
+            W, Cm, _ = t.download_model()
+            t.close()
+            E = Cm if G.eval_matrix(name) == 1 else W
+            runs.append(scores(words, E, qs, prs, torch.device("cuda", 0)))
+            del W, Cm, E
+        got.append(np.mean(runs, 0))
+    got = np.array(got).mean(0)
+    d_seq = got - refs[0]
+    d_omp = got - refs[-1] if len(refs) > 1 else np.array([np.nan, np.nan])
+    print(f"headline-scale {name} ({w['mode']} d{w['dim']}, V {counts.size}, {raw} tokens): gpu {got.round(2)} "
+          f"sequential {refs[0].round(2)} omp16 {refs[-1].round(2) if len(refs) > 1 else None} delta vs sequential "
+          f"{d_seq.round(2)} vs omp16 {d_omp.round(2)} policy {pol}")
     for k, metric in enumerate(("analogy", "similarity")):
-        lo, hi = HEADLINE_BOUNDS[name][metric]
-        assert lo <= dl[k] <= hi, (name, metric, dl[k], (lo, hi), got, ref)
+        lo, hi = band[metric]
+        assert got[k] >= lo - 1.0, (name, metric, "below the reference by more than a point", got, refs)
+        dev = DEVIATION_HIGH.get(name, {}).get(metric)
+        top = refs[0][k] + dev if dev is not None else hi + 1.0
+        assert got[k] <= top, (name, metric, "above the bound", got, refs, top)

@@ -85,6 +85,7 @@ struct Knobs {
   double ctx_avg = -1;           // W2V_CTX_AVG: private_average of the CBOW context rows (0 = plain sum)
   double priv_hs_tail_avg = -1;  // W2V_PRIV_HS_TAIL_AVG: private_average of the HS nodes past the 64th
   double hs_hot_avg = -1;        // W2V_HS_HOT_AVG: concurrent updates the atomic hot HS nodes' deltas are scaled to (0 = none)
+  int wide_hs = -1;              // W2V_WIDE_HS=0: large-vocabulary HS keeps the round-5 policy (experiments)
   std::string desc;             // "NAME=value ..." of the variables that were set
 };
 
@@ -108,6 +109,7 @@ static Knobs read_knobs() {
   if (const char* v = get("W2V_CTX_AVG")) k.ctx_avg = std::max(0.0, std::atof(v));
   if (const char* v = get("W2V_PRIV_HS_TAIL_AVG")) k.priv_hs_tail_avg = std::max(0.0, std::atof(v));
   if (const char* v = get("W2V_HS_HOT_AVG")) k.hs_hot_avg = std::max(0.0, std::atof(v));
+  if (const char* v = get("W2V_WIDE_HS")) k.wide_hs = std::atoi(v) != 0;
   return k;
 }
 
@@ -671,6 +673,40 @@ int w2v_dev_download_model(w2v_dev* h, float* W, float* C, float* S) {
 }
 
 namespace w2v {
+// max |A - B| and max |A| over the first d columns of two pitch-padded
+// matrices (non-negative floats compare as their bits: one 32-bit atomicMax
+// per block each).
+__global__ void max_diff_kernel(const float* A, const float* B, int64_t rows, int64_t pitch, int d,
+                                unsigned int* out) {
+  __shared__ unsigned int part[2][4];
+  float dm = 0.f, am = 0.f;
+  const int64_t n = rows * (int64_t)d;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = k / d, c = k - r * d;
+    const float a = A[r * pitch + c], b = B[r * pitch + c];
+    dm = fmaxf(dm, fabsf(a - b));
+    am = fmaxf(am, fabsf(a));
+    if (!(a == a) || !(b == b)) dm = __int_as_float(0x7F800000);  // NaN counts as infinitely different
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    dm = fmaxf(dm, __shfl_xor(dm, o));
+    am = fmaxf(am, __shfl_xor(am, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    part[0][threadIdx.x >> 6] = __float_as_uint(dm);
+    part[1][threadIdx.x >> 6] = __float_as_uint(am);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned int x = 0, y = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+      x = max(x, part[0][w]);
+      y = max(y, part[1][w]);
+    }
+    atomicMax(out, x);
+    atomicMax(out + 1, y);
+  }
+}
 // rows[k] of M (pitch-padded) <-> packed[k] (dim floats), one wave per row.
 __global__ void scatter_rows_kernel(float* M, int64_t pitch, int d, const int32_t* rows, int64_t n, const float* packed) {
   const int64_t k = blockIdx.x;
@@ -687,6 +723,57 @@ __global__ void gather_rows_kernel(const float* M, int64_t pitch, int d, const i
   for (int e = threadIdx.x; e < d; e += blockDim.x) dst[e] = src[e];
 }
 }  // namespace w2v
+
+int w2v_dev_model_max_diff(w2v_dev* a, w2v_dev* b, float* out) {
+  if (!a || !b || !out) return fail(W2V_ERR_ARG, "null argument");
+  if (!a->W || !b->W) return fail(W2V_ERR_STATE, "no model on the device");
+  if (a->V != b->V || a->pitch != b->pitch || a->cfg.word_dim != b->cfg.word_dim || !a->C != !b->C ||
+      !a->S != !b->S)
+    return fail(W2V_ERR_ARG, "the two handles hold models of different shapes");
+  if (set_device(b)) return W2V_ERR_HIP;
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  if (set_device(a)) return W2V_ERR_HIP;
+  HIP_TRY(hipStreamSynchronize(a->stream));
+  const float* MA[3] = {a->W, a->C, a->S};
+  const float* MB[3] = {b->W, b->C, b->S};
+  const int64_t rows[3] = {a->V, a->V, a->V - 1};
+  unsigned int* acc = nullptr;
+  float* stage = nullptr;  // b's matrix on a's device when they differ
+  int rc = W2V_OK;
+  if (hipMalloc(&acc, 6 * sizeof(unsigned int)) != hipSuccess) return fail(W2V_ERR_HIP, "max_diff: hipMalloc");
+  if (hipMemset(acc, 0, 6 * sizeof(unsigned int)) != hipSuccess) rc = fail(W2V_ERR_HIP, "max_diff: memset");
+  for (int k = 0; k < 3 && rc == W2V_OK; ++k) {
+    if (!MA[k] || rows[k] <= 0) continue;
+    const size_t bytes = (size_t)rows[k] * (size_t)a->pitch * sizeof(float);
+    const float* B = MB[k];
+    if (a->device != b->device) {
+      if (!stage && hipMalloc(&stage, (size_t)a->V * (size_t)a->pitch * sizeof(float)) != hipSuccess) {
+        rc = fail(W2V_ERR_HIP, "max_diff: staging buffer");
+        break;
+      }
+      if (hipMemcpyPeer(stage, a->device, B, b->device, bytes) != hipSuccess) {
+        rc = fail(W2V_ERR_HIP, "max_diff: peer copy");
+        break;
+      }
+      B = stage;
+    }
+    hipLaunchKernelGGL(w2v::max_diff_kernel, dim3(2048), dim3(256), 0, a->stream, MA[k], B, rows[k], a->pitch,
+                       a->cfg.word_dim, acc + 2 * k);
+    if (hipGetLastError() != hipSuccess) rc = fail(W2V_ERR_HIP, "max_diff_kernel launch");
+    if (rc == W2V_OK && hipStreamSynchronize(a->stream) != hipSuccess) rc = fail(W2V_ERR_HIP, "max_diff sync");
+  }
+  unsigned int host[6] = {0, 0, 0, 0, 0, 0};
+  if (rc == W2V_OK && hipMemcpy(host, acc, sizeof(host), hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(W2V_ERR_HIP, "max_diff copy");
+  (void)hipFree(acc);
+  if (stage) (void)hipFree(stage);
+  for (int k = 0; k < 6; ++k) {
+    float f;
+    std::memcpy(&f, &host[k], sizeof(f));
+    out[k] = f;
+  }
+  return rc;
+}
 
 // Row-sparse transfer between host rows and one resident matrix: the per-call
 // methods (train_sentence_*) move only the rows a sentence's update can touch.
@@ -1125,6 +1212,31 @@ static double private_rate_for(const w2v_dev* h, int64_t count, int64_t max_wave
 // rows = 58; configs[0] 4, configs[1] 1.2, configs[2] 0.4) and holds the
 // r04a input's skip-gram at 9 waves.
 constexpr double kPairPressure = 64.0;
+
+// Hierarchical softmax on a large vocabulary (V >= kWidePrivVocab, round 6):
+// no LDS-private Huffman nodes or context rows, and the waves in flight
+// capped so that the root — every update's first node — has at most
+// kHsRootPressure updates in flight (waves x its expected updates per kept
+// center: skip-gram window + 1, one per context; CBOW 1): plain Hogwild at
+// the reference's own granularity, the atomic hot nodes exact. The round-5
+// policy (127 private nodes flushed as a damped mean) scored 13-19 analogy
+// points BELOW the sequential reference at configs[2]'s scale (SG-HS
+// -18.2 / -0.2, CBOW-HS -5.3..-13.3 / -1.1..-1.2; profiles/r05ba_*, r05be_*,
+// r06a_*, r06b_*), and no damping of the nodes closes it (the hot nodes'
+// deltas scaled to 64 / 16 / 4 / 1 concurrent contributions: -5.4 / +36.5 /
+// +40.8 / +4.4, r06a_2_*). Without private nodes (r06a_2_*, r06b_*, r06c_*):
+// SG-HS -14.9 at all 8 K waves, -5.2 / -4.2 / -0.54 at 2048 / 512 / 256;
+// CBOW-HS -12.5 / -9.9 at 1024 / 256 with private context rows, +1.54 / +0.73
+// at 1536 / 256 without. 256 (skip-gram) and 1536 (CBOW) waves are both
+// 1536 root updates in flight. Text8-sized vocabularies keep the private
+// nodes: there the same rule costs SG-HS 3 analogy points (c1hs, 256 waves:
+// -2.97) and configs[1]'s CBOW-HS its throughput.
+constexpr double kHsRootPressure = 1536.0;
+static bool wide_hs_rule(const w2v_dev* h) {
+  return h->cfg.hs && h->V >= kWidePrivVocab && h->sched == W2V_SCHED_PARALLEL &&
+         h->update == W2V_UPDATE_PER_PAIR && h->knobs.wide_hs != 0;
+}
+
 static int64_t effective_max_waves(w2v_dev* h, int64_t count) {
   if (h->max_waves > 0) return h->max_waves;
   if (h->sched != W2V_SCHED_PARALLEL || h->update != W2V_UPDATE_PER_PAIR) return 0;
@@ -1135,7 +1247,12 @@ static int64_t effective_max_waves(w2v_dev* h, int64_t count) {
   const double T = h->cfg.cbow ? win1 + ns + (h->cfg.hs ? h->path_len_fk : 0.0)
                                : 1.0 + win1 * (ns + (h->cfg.hs ? h->path_len_f : 0.0));
   if (!(T > 0.0)) return 0;
-  const double cap = std::floor(kPairPressure * (double)h->V / T);
+  double cap = std::floor(kPairPressure * (double)h->V / T);
+  if (wide_hs_rule(h) && (int64_t)h->node_f.size() == h->V - 1) {
+    const int64_t root = h->V - 2;
+    const double m = h->cfg.cbow ? h->node_fk[(size_t)root] : win1 * h->node_f[(size_t)root];
+    if (m > 0.0) cap = std::min(cap, std::floor(kHsRootPressure / m));
+  }
   const int64_t per_simd = h->nv <= 2 ? 8 : 4;  // kMinWaves<NV>
   const int64_t chip = (int64_t)h->n_cu * 4 * per_simd;
   // The waves the launch would run: min(chip, count) with count in sentences
@@ -1433,7 +1550,8 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     const int64_t auto_rows = sg_hs ? w2v::kPrivMax
                               : !sg_ns ? (wide_hs ? kCbowHsPrivNodes : 64)
                                        : h->V >= kWidePrivVocab ? w2v::kPrivMax : kSgNsPrivRows;
-    int64_t P = std::min<int64_t>(fit, h->private_rows > 0 ? w2v::kPrivMax : auto_rows);
+    const bool plain_hs = wide_hs_rule(h);  // large-vocabulary HS: no LDS-private nodes / context rows
+    int64_t P = std::min<int64_t>(fit, h->private_rows > 0 ? w2v::kPrivMax : plain_hs ? 0 : auto_rows);
     if (h->private_rows >= 0) P = std::min<int64_t>(P, h->private_rows);
     const bool hs = h->cfg.hs != 0;
     const int64_t avail = hs ? h->V - 1 : h->V;
@@ -1465,6 +1583,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     // and 5.8x on configs[1]'s at d200 / negative 5 (106 -> 613 M; r05v_2_*, r05v_3_*).
     int64_t Q = h->cfg.cbow ? std::min<int64_t>({fit - P, (int64_t)w2v::kCtxMax, h->V}) : 0;
     if (h->context_rows >= 0) Q = std::min<int64_t>(Q, h->context_rows);
+    else if (plain_hs) Q = 0;
     else if (rate > 0.0) Q = std::min(Q, by_rate.second);
     if (Q > 0) {
       a.ctx_M = h->C;

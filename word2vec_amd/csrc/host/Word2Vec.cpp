@@ -7,6 +7,7 @@
 #include "Word2Vec.h"
 
 #include <algorithm>
+#include <limits>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -581,6 +582,8 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
     epochs_done_ = first;
     resume_ = false;
     epoch_seconds.clear();
+    replica_rounds = 0;
+    replica_max_diff = -1.0;
     for (int it = 0; it < iter; ++it) {
       std::shuffle(sample_idx.begin(), sample_idx.end(), generator);  // :373
       if (it < first) continue;  // done before the checkpoint
@@ -638,6 +641,22 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
       }
     }
     cur_words_ = global;
+    {
+      int32_t nr = 0, loc = 0, ov = 0;
+      int64_t rounds = 0;
+      check(w2v_group_info(grp, &nr, &loc, &ov, &rounds), "w2v_group_info");
+      replica_rounds = rounds;
+      // the replicas' models after the last fold, relative to their magnitude:
+      // equal up to the fp32 rounding of M + (s A - D) across the rounds
+      replica_max_diff = 0.0;
+      for (size_t i = 1; i < R; ++i) {
+        float o[6] = {0, 0, 0, 0, 0, 0};
+        check(w2v_dev_model_max_diff(reps[i], reps[0], o), "w2v_dev_model_max_diff");
+        for (int k = 0; k < 3; ++k)
+          if (o[3 + k] > 0.0f) replica_max_diff = std::max(replica_max_diff, (double)o[k] / (double)o[3 + k]);
+          else if (o[k] > 0.0f) replica_max_diff = std::numeric_limits<double>::infinity();
+      }
+    }
     check(w2v_dev_download_model(reps[0], W.data(), uses_C() ? C.data() : nullptr,
                                  train_method == "hs" ? synapses1.data() : nullptr),
           "w2v_dev_download_model");

@@ -262,6 +262,8 @@ int w2v_model_load_checkpoint(w2v_model* m, const char* path) {
   return guard(m, [&] { m->w.load_checkpoint(path); });
 }
 int64_t w2v_model_current_words(w2v_model* m) { return m->w.current_words(); }
+int64_t w2v_model_replica_rounds(w2v_model* m) { return m->w.replica_rounds; }
+double w2v_model_replica_max_diff(w2v_model* m) { return m->w.replica_max_diff; }
 int w2v_model_set_checkpoint_path(w2v_model* m, const char* path) {
   return guard(m, [&] { m->w.checkpoint_path = path ? path : ""; });
 }

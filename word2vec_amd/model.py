@@ -71,6 +71,8 @@ def _load():
             "w2v_model_epochs_done": (I64, [P]),
             "w2v_model_epoch_seconds": (C.c_double, [P, I64]),
             "w2v_model_current_words": (I64, [P]),
+            "w2v_model_replica_rounds": (I64, [P]),
+            "w2v_model_replica_max_diff": (C.c_double, [P]),
             "w2v_model_read_vocab": (C.c_int, [P, S]),
         }
         for k, (r, a) in sig.items():
@@ -219,6 +221,16 @@ class Word2Vec:
         while (t := self.L.w2v_model_epoch_seconds(self.h, len(out))) >= 0:
             out.append(t)
         return out
+
+    @property
+    def replica_rounds(self) -> int:
+        """Exchanges the replicas (gpu_devices) ran in the last train call."""
+        return self.L.w2v_model_replica_rounds(self.h)
+
+    @property
+    def replica_max_diff(self) -> float:
+        """max |M_i - M_0| / max |M_0| over the replicas after the last exchange (-1: not measured)."""
+        return self.L.w2v_model_replica_max_diff(self.h)
 
     @property
     def current_words(self) -> int:
