@@ -47,10 +47,12 @@ MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X dense f32-input MFMA (MI355X_MICROARCH.md
 # cadence and in that mode — what the product runs on that workload.
 CONFIG3_TOKENS = 10_000_000_000
 AUTO_ROUNDS, AUTO_AVERAGE_WORDS, AUTO_AVERAGE_REPLICAS = 64, 4_000_000, 4  # include/Word2Vec.h
+AUTO_ADAPTIVE_ROUNDS = 128  # Word2Vec::kAutoAdaptiveRounds: the adaptive divisor's cadence
 
 
-def config3_sync_words(world):
-    return CONFIG3_TOKENS // max(1, world) // AUTO_ROUNDS
+def config3_sync_words(world, mode="adaptive"):
+    rounds = AUTO_ADAPTIVE_ROUNDS if mode == "adaptive" else AUTO_ROUNDS
+    return CONFIG3_TOKENS // max(1, world) // rounds
 
 
 def auto_replica_mode(world, shard_words=None):
@@ -273,7 +275,7 @@ def main():
     if args.sync_every > 0 or world == 1:
         rounds = n_rounds(n_sent * world, world, args.sync_every)
     else:  # every rank's shard has ~ the same words: the same round count everywhere
-        rounds = max(1, -(-int(ids_h.size) // max(1, args.sync_words or config3_sync_words(world))))
+        rounds = max(1, -(-int(ids_h.size) // max(1, args.sync_words or config3_sync_words(world, rmode))))
     order_dev = torch.arange(n_sent, dtype=torch.int64, device=dev)  # this rank's shard, in order
     round_words = global_round_words(local_round_words(soff_h, range(n_sent), rounds), world)
     progress = 0

@@ -169,6 +169,10 @@ class Word2Vec {
   bool overlap_average = true;
   int replica_mode = -1;
   static const int64_t kAutoReplicaRounds = 64;  // 2 replicas within a point at 32-64 per epoch
+  // ... and for the adaptive divisor (more than two replicas of short
+  // shards): eight replicas of configs[3]'s shape lost 1.96 similarity points
+  // at 64 exchanges per epoch, 0.13-0.64 at 96-128
+  static const int64_t kAutoAdaptiveRounds = 128;
   // sync_words = 0 with replica_mode W2V_GROUP_AVERAGE: at most one exchange
   // per this many words of a shard, so each round's mean spans rows every
   // replica trained

@@ -40,7 +40,9 @@ def test_replica_auto_matches_the_class(monkeypatch):
     assert [mod.auto_replica_mode(n) for n in (2, 4, 8)] == ["average", "average", "adaptive"]
     assert mod.auto_replica_mode(2, 200_000_000) == "sum"  # short shards: the sum for two
     assert mod.auto_replica_mode(3, 200_000_000) == "adaptive"
-    assert mod.config3_sync_words(8) == 10_000_000_000 // 8 // 64
+    assert mod.config3_sync_words(8) == 10_000_000_000 // 8 // 128  # the adaptive divisor's cadence
+    assert mod.config3_sync_words(4, "average") == 10_000_000_000 // 4 // 64
     hdr = (ROOT / "include" / "Word2Vec.h").read_text()
     assert "kAutoReplicaRounds = 64;" in hdr and "kAutoAverageWords = 4000000;" in hdr
+    assert "kAutoAdaptiveRounds = 128;" in hdr
     assert "kAutoAverageReplicas = 4;" in hdr

@@ -767,10 +767,9 @@ int w2v_dev_model_max_diff(w2v_dev* a, w2v_dev* b, float* out) {
     rc = fail(W2V_ERR_HIP, "max_diff copy");
   (void)hipFree(acc);
   if (stage) (void)hipFree(stage);
-  for (int k = 0; k < 6; ++k) {
-    float f;
-    std::memcpy(&f, &host[k], sizeof(f));
-    out[k] = f;
+  for (int k = 0; k < 3; ++k) {  // acc holds (max |A - B|, max |A|) per matrix
+    std::memcpy(&out[k], &host[2 * k], sizeof(float));
+    std::memcpy(&out[3 + k], &host[2 * k + 1], sizeof(float));
   }
   return rc;
 }

@@ -574,7 +574,7 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
     const int mode = replica_mode >= 0 ? replica_mode
                      : (R <= (size_t)kAutoAverageReplicas && long_shards) ? W2V_GROUP_AVERAGE
                      : R <= 2 ? W2V_GROUP_SUM : W2V_GROUP_ADAPTIVE;
-    const int64_t auto_rounds = kAutoReplicaRounds;
+    const int64_t auto_rounds = mode == W2V_GROUP_ADAPTIVE ? kAutoAdaptiveRounds : kAutoReplicaRounds;
     check(w2v_group_set_mode(grp, mode), "w2v_group_set_mode");
     std::vector<long> sample_idx((size_t)n);
     std::iota(sample_idx.begin(), sample_idx.end(), 0);
@@ -599,7 +599,8 @@ void Word2Vec::run_epochs_replicas(const std::vector<int32_t>& ids, const std::v
         largest = std::max(largest, cum[i].back());
         check(w2v_dev_set_order(reps[i], shard[i].data(), (int64_t)shard[i].size()), "w2v_dev_set_order");
       }
-      // auto cadence: kAutoReplicaRounds per epoch; plain averaging wants
+      // auto cadence: kAutoReplicaRounds per epoch (kAutoAdaptiveRounds for
+      // the adaptive divisor); plain averaging wants
       // LONG rounds — a round's mean divides the progress of every row only
       // one replica touched in it by R — so with W2V_GROUP_AVERAGE at most
       // one exchange per kAutoAverageWords words of a shard

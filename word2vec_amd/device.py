@@ -104,6 +104,12 @@ class DeviceTrainer:
         arrs = [None if a is None else np.ascontiguousarray(a, dtype=np.float32).reshape(-1, d) for a in (W, C_, S)]
         self._chk(self.lib.w2v_dev_upload_model(self.h, *[_ptr(a) for a in arrs]), "w2v_dev_upload_model")
 
+    def max_diff(self, other) -> dict:
+        """w2v_dev_model_max_diff: per matrix (max |self - other|, max |self|)."""
+        out = (C.c_float * 6)()
+        self._chk(self.lib.w2v_dev_model_max_diff(self.h, other.h, out), "w2v_dev_model_max_diff")
+        return {k: (out[i], out[3 + i]) for i, k in enumerate(("W", "C", "S"))}
+
     def download_model(self):
         d, V = self.cfg.word_dim, self.V
         W = np.empty((V, d), np.float32)
