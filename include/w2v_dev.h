@@ -303,6 +303,10 @@ int w2v_dev_private_rate_used(w2v_dev* h, float* mu);
  * window 150 / negative 80 diverges from 128 waves up, as the reference's own
  * OpenMP loop does on 8 threads). Every benchmarked shape stays uncapped. */
 int w2v_dev_wave_cap_used(w2v_dev* h, int64_t* waves);
+/* 1 if the last launch ran the low-occupancy deep-pipeline HS kernel (the
+ * large-vocabulary HS policy's capped launches; environment W2V_DEEP_HS=1
+ * forces it for any HS launch without negatives, 0 disables it). */
+int w2v_dev_deep_used(w2v_dev* h, int32_t* deep);
 /* The replica count the update policy assumes (no reference counterpart: the
  * reference trains one model). w2v_group_create sets it to the group's ranks;
  * the one-GPU rehearsal of an N-rank run (each rank a one-rank group, the

@@ -62,6 +62,37 @@ def _run_replay(mode, sentences, dim, window, iters, table_size=100_000, cbow_me
     return got, want, init
 
 
+# The low-occupancy deep-pipeline HS kernel (train_epoch_deep_kernel, round 6:
+# the large-vocabulary HS policy's capped launches) gathers a Huffman path
+# 8-16 nodes at a time instead of 4; forced on the sequential Philox schedule
+# (W2V_DEEP_HS=1, read at w2v_dev_create) it must train what the oracle does,
+# at every row width it serves (NV <= 12).
+@pytest.mark.parametrize("mode", ["sg_hs", "cbow_hs"])
+@pytest.mark.parametrize("dim", [40, 100, 200, 300, 512, 700])
+def test_philox_sequential_deep_hs(mode, dim, monkeypatch):
+    sents = zipf_sentences(8, 160, 300, seed=41, ragged=True)
+    o = oracle_run(sents, mode, dim=dim, window=5, iters=1, table_size=100_000, train=False)
+    o.build_sample()
+    cfg = device_config(o, mode, dim, 5, 1, 100_000, True, 0.05, 2.5e-6)
+    monkeypatch.setenv("W2V_DEEP_HS", "1")
+    d = device_from_oracle(o, cfg, initial=False)
+    monkeypatch.delenv("W2V_DEEP_HS")
+    init = [o.matrix(k) for k in range(3)]
+    key = 0x0DEE_9000_0000_0001 + dim
+    order = np.random.default_rng(dim).permutation(o.samples()[1].size - 1)
+    o.train_philox(0, 1, order, key, 0)
+    d.set_rng(N.W2V_RNG_PHILOX, key)
+    d.set_schedule(N.W2V_SCHED_SEQUENTIAL)
+    d.set_progress(0)
+    st = d.train_epoch(0, order)
+    assert d.policy()["deep"] == 1
+    assert st["words"] == o.current_words
+    got = d.download_model()
+    want = [o.matrix(k) if got[k] is not None else None for k in range(3)]
+    check_parity(got, want, init, *MULTI, tag=f"philox deep {mode} d{dim}")
+    d.close()
+
+
 @pytest.mark.parametrize("mode", list(MODES))
 @pytest.mark.parametrize("dim", [48, 100, 200, 300, 512])
 def test_replay_single_sentence(mode, dim):

@@ -119,6 +119,7 @@ SIGNATURES = {
     "w2v_dev_hot_tau": (C.c_int, [_P, C.POINTER(_F), C.POINTER(_F)]),
     "w2v_dev_private_rate_used": (C.c_int, [_P, C.POINTER(_F)]),
     "w2v_dev_wave_cap_used": (C.c_int, [_P, C.POINTER(_I64)]),
+    "w2v_dev_deep_used": (C.c_int, [_P, C.POINTER(_I32)]),
     "w2v_dev_set_replica_count": (C.c_int, [_P, _I32]),
     "w2v_dev_model_max_diff": (C.c_int, [_P, _P, C.POINTER(_F)]),
     "w2v_dev_replica_count": (C.c_int, [_P, C.POINTER(_I32)]),

@@ -86,6 +86,7 @@ struct Knobs {
   double priv_hs_tail_avg = -1;  // W2V_PRIV_HS_TAIL_AVG: private_average of the HS nodes past the 64th
   double hs_hot_avg = -1;        // W2V_HS_HOT_AVG: concurrent updates the atomic hot HS nodes' deltas are scaled to (0 = none)
   int wide_hs = -1;              // W2V_WIDE_HS=0: large-vocabulary HS keeps the round-5 policy (experiments)
+  int deep_hs = -1;              // W2V_DEEP_HS: 1 forces the deep-pipeline HS kernel, 0 never (auto: capped HS launches)
   std::string desc;             // "NAME=value ..." of the variables that were set
 };
 
@@ -110,6 +111,7 @@ static Knobs read_knobs() {
   if (const char* v = get("W2V_PRIV_HS_TAIL_AVG")) k.priv_hs_tail_avg = std::max(0.0, std::atof(v));
   if (const char* v = get("W2V_HS_HOT_AVG")) k.hs_hot_avg = std::max(0.0, std::atof(v));
   if (const char* v = get("W2V_WIDE_HS")) k.wide_hs = std::atoi(v) != 0;
+  if (const char* v = get("W2V_DEEP_HS")) k.deep_hs = std::atoi(v) != 0;
   return k;
 }
 
@@ -206,6 +208,7 @@ struct w2v_dev {
   int32_t last_priv = 0, last_ctx = 0;
   int32_t last_flush = 0, last_ctx_flush = 0;
   double last_hs_hot_avg = 0.0;     // the hot-node average of the last launch (0: none)
+  bool last_deep = false;           // the last launch ran train_epoch_deep_kernel
   // per atomic hot Huffman node [hot_s, V - 1): the scale of its deltas (hot_node_scales)
   std::vector<float> hot_sc_h;
   float* hot_sc_d = nullptr;
@@ -326,6 +329,23 @@ KernelFn kernel_for(const w2v_dev* h) {
     case 16: return w2v::pick_train_nv16(cb, hs, ns, rp, wd);
     case 24: return w2v::pick_train_nv24(cb, hs, ns, rp, wd);
     default: return w2v::pick_train_nv32(cb, hs, ns, rp, wd);
+  }
+}
+
+KernelFn kernel_deep_for(const w2v_dev* h) {
+  const bool cb = h->cfg.cbow != 0;
+  switch (h->nv) {
+    case 1: return w2v::pick_train_deep_nv1(cb);
+    case 2: return w2v::pick_train_deep_nv2(cb);
+    case 3: return w2v::pick_train_deep_nv3(cb);
+    case 4: return w2v::pick_train_deep_nv4(cb);
+    case 5: return w2v::pick_train_deep_nv5(cb);
+    case 6: return w2v::pick_train_deep_nv6(cb);
+    case 8: return w2v::pick_train_deep_nv8(cb);
+    case 12: return w2v::pick_train_deep_nv12(cb);
+    case 16: return w2v::pick_train_deep_nv16(cb);
+    case 24: return w2v::pick_train_deep_nv24(cb);
+    default: return w2v::pick_train_deep_nv32(cb);
   }
 }
 
@@ -1502,6 +1522,17 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     wpb = 1;
     while (wpb * 2 <= max_wpb && wpb * 2 <= per) wpb *= 2;
   }
+  // The low-occupancy deep-pipeline kernel (train_epoch_deep_kernel) for a
+  // capped HS launch (<= 4 waves per workgroup; W2V_DEEP_HS=1 forces it for
+  // any HS launch without negatives, sequential schedules included: parity
+  // tests; 0 never)
+  const bool deep_ok = h->cfg.hs && h->cfg.negative <= 0 && h->rng != W2V_RNG_REPLAY && h->nv <= 12 &&
+                       !(h->cfg.cbow && 2 * h->cfg.window + 1 > w2v::kWave) && !sn_fn;
+  const bool deep = deep_ok && (h->knobs.deep_hs == 1 ||
+                                (h->knobs.deep_hs != 0 && h->sched == W2V_SCHED_PARALLEL && max_waves > 0 &&
+                                 wpb * w2v::kWave <= w2v::kDeepBlock));
+  if (deep) wpb = std::min(wpb, w2v::kDeepBlock / w2v::kWave);
+  h->last_deep = deep;
   // Flush interval of the privatised rows, in centers of the workgroup (about
   // 64 centers per wave for NS, 4 per wave for HS whose top nodes every
   // update touches), and the averaging of their deltas (flush_private). A
@@ -1689,17 +1720,20 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     HIP_TRY(hipGetLastError());
     return W2V_OK;
   }
-  KernelFn fn = kernel_for(h);
+  const KernelFn occ_fn = kernel_for(h);  // the hot-row rule counts the regular kernel's residency
+  KernelFn fn = deep ? kernel_deep_for(h) : occ_fn;
   HIP_TRY(hipMemsetAsync(h->work, 0, sizeof(unsigned int), h->stream));
   dim3 grid(1), block(64);
   int64_t resident_waves = 1, resident_wg = 1;
   if (h->sched == W2V_SCHED_PARALLEL) {
     const int threads = wpb * w2v::kWave;
-    int per_cu = 0;
+    int per_cu = 0, per_cu_occ = 0;
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds_bytes));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_occ, occ_fn, threads, lds_bytes));
     if (per_cu < 1) per_cu = 1;
+    if (per_cu_occ < 1) per_cu_occ = 1;
     const int64_t resident = (int64_t)per_cu * h->n_cu;
-    resident_waves = (int64_t)per_cu * h->n_cu * (max_wpb);
+    resident_waves = (int64_t)per_cu_occ * h->n_cu * (max_wpb);
     resident_wg = resident;
     const int64_t need = (count + wpb - 1) / wpb;
     int64_t g = need < resident ? need : resident;
@@ -1946,6 +1980,12 @@ int w2v_dev_private_rate_used(w2v_dev* h, float* mu) {
 int w2v_dev_wave_cap_used(w2v_dev* h, int64_t* waves) {
   if (!h) return fail(W2V_ERR_ARG, "null handle");
   if (waves) *waves = h->last_wave_cap;
+  return W2V_OK;
+}
+
+int w2v_dev_deep_used(w2v_dev* h, int32_t* deep) {
+  if (!h || !deep) return fail(W2V_ERR_ARG, "null argument");
+  *deep = h->last_deep ? 1 : 0;
   return W2V_OK;
 }
 

@@ -32,6 +32,14 @@ KernelFn W2V_CAT(pick_train_nv, W2V_NV)(bool cbow, bool hs, bool ns, bool replay
 #undef W2V_K
 }
 
+// hierarchical softmax without negatives (the large-vocabulary HS policy's
+// capped launches): the low-occupancy, deep-pipeline kernel
+KernelFn W2V_CAT(pick_train_deep_nv, W2V_NV)(bool cbow) {
+  constexpr int M = kDeepMaxT<W2V_NV>;
+  return cbow ? &train_epoch_deep_kernel<W2V_NV, M, true, true, false, false, false>
+              : &train_epoch_deep_kernel<W2V_NV, M, false, true, false, false, false>;
+}
+
 ApplyFn W2V_CAT(pick_apply_nv, W2V_NV)() { return &apply_rows_kernel<W2V_NV>; }
 
 }  // namespace w2v

@@ -598,6 +598,33 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
+// A batch of N > 8 targets (the deep HS pipeline of the low-occupancy
+// kernel, train_epoch_deep_kernel) in groups of 8: group h's dots are folded
+// and evaluated exactly as a batch of 8 would be (batch_dots / batch_grad_l),
+// so each target's sum, sigma and g are the bits a batch of <= 8 gives. For N
+// <= 8 this is the single batch_dots + batch_grad_l of before.
+template <int N>
+constexpr int kGroups = (N + 7) / 8;
+template <int N>
+constexpr int kGroupN = N < 8 ? N : 8;
+template <int N, bool HSF>
+__device__ __forceinline__ void batch_g(const float (&pd)[N], int T, int code_l, int c0, float alpha, int lane,
+                                        unsigned long long* stats, float (&gl)[kGroups<N>]) {
+  constexpr int G = kGroupN<N>;
+#pragma unroll
+  for (int h = 0; h < kGroups<N>; ++h) {
+    float q[G];
+#pragma unroll
+    for (int t = 0; t < G; ++t) q[t] = (8 * h + t < N) ? pd[8 * h + t] : 0.f;
+    gl[h] = batch_grad_l<G, HSF>(batch_dots<G>(q, lane), T - 8 * h, code_l, c0 + 8 * h, alpha, lane, stats);
+  }
+}
+// g of target t from batch_g's per-group lanes
+template <int N>
+__device__ __forceinline__ float batch_gt(const float (&gl)[kGroups<N>], int t) {
+  return readlane_f(gl[t / 8], batch_lane<kGroupN<N>>(t % 8));
+}
+
 // ---------------------------------------------------------------------------
 // The per-target update (Word2Vec.cpp:238-246 HS; :261-268 NS), for up to
 // MAXT distinct rows at once. Lane (t0 + t) of row_l / code_l holds target t's
@@ -637,7 +664,8 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
       for (int v = 1; v < NV; ++v) pd[t] += r[t][v] * x[v];
     }
   }
-  const float g_l = batch_grad_l<MAXT, HSF>(batch_dots<MAXT>(pd, lane), T, code_l, t0, alpha, lane, stats);
+  float g_l[kGroups<MAXT>];
+  batch_g<MAXT, HSF>(pd, T, code_l, t0, alpha, lane, stats, g_l);
 #else
   float f[MAXT];
 #pragma unroll
@@ -656,7 +684,7 @@ __device__ __forceinline__ void apply_targets(float* M, int64_t pitch, int d, in
   for (int t = 0; t < MAXT; ++t) {
     if (t < T) {
 #if W2V_BATCH_DOTS
-      const float gt = readlane_f(g_l, batch_lane<MAXT>(t));
+      const float gt = batch_gt<MAXT>(g_l, t);
 #else
       if (stats) note_nonfinite(stats, !__builtin_isfinite(f[t]), lane);
       const float gt = readlane_f(g_l, t);
@@ -778,7 +806,8 @@ __device__ __forceinline__ void hs_score(const TrainArgs& a, int T, int row_l, i
       for (int v = 1; v < NV; ++v) pd[t] += r[t][v] * x[v];
     }
   }
-  const float g_l = batch_grad_l<MT, true>(batch_dots<MT>(pd, lane), T, code_l, t0, alpha, lane, a.stats);
+  float g_l[kGroups<MT>];
+  batch_g<MT, true>(pd, T, code_l, t0, alpha, lane, a.stats, g_l);
 #else
   float f[MT];
 #pragma unroll
@@ -798,7 +827,7 @@ __device__ __forceinline__ void hs_score(const TrainArgs& a, int T, int row_l, i
     gt[t] = 0.f;
     if (t < T) {
 #if W2V_BATCH_DOTS
-      gt[t] = readlane_f(g_l, batch_lane<MT>(t));
+      gt[t] = batch_gt<MT>(g_l, t);
 #else
       note_nonfinite(a.stats, !__builtin_isfinite(f[t]), lane);
       gt[t] = readlane_f(g_l, t);
@@ -1488,7 +1517,7 @@ __device__ __forceinline__ void center(const TrainArgs& a, float* lds, const int
 // The epoch kernel: wavefronts dequeue sentences (Word2Vec.cpp:375-394).
 // ---------------------------------------------------------------------------
 template <int NV, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY, bool WIDE>
-__global__ __launch_bounds__(kMaxBlock<NV>, kMinWaves<NV>) void train_epoch_kernel(TrainArgs a) {
+__device__ __forceinline__ void train_epoch(const TrainArgs& a) {
   extern __shared__ float w2v_lds[];
   const int lane = lane_id();
   float* lds = (a.priv_n + a.ctx_n) > 0 ? w2v_lds : nullptr;
@@ -1590,6 +1619,25 @@ __global__ __launch_bounds__(kMaxBlock<NV>, kMinWaves<NV>) void train_epoch_kern
     atomicAdd(&a.stats[3], cnt.draws);
     atomicAdd(&a.stats[4], cnt.sentences);
   }
+}
+
+template <int NV, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY, bool WIDE>
+__global__ __launch_bounds__(kMaxBlock<NV>, kMinWaves<NV>) void train_epoch_kernel(TrainArgs a) {
+  train_epoch<NV, MAXT, CBOW, HS, NS, REPLAY, WIDE>(a);
+}
+
+// The same epoch for a launch that runs few waves (round 6: large-vocabulary
+// HS capped at kHsRootPressure root updates in flight, 1-6 waves per CU):
+// workgroups of <= 4 waves and a 256-VGPR budget (2 waves per SIMD), so a
+// Huffman path is gathered kDeepMaxT / 2 nodes at a time instead of 4 —
+// a wave that has the CU to itself is latency-bound on its path's round
+// trips. Same arithmetic in the same order as train_epoch_kernel.
+template <int NV>
+constexpr int kDeepMaxT = NV <= 2 ? 32 : NV <= 4 ? 24 : NV <= 6 ? 16 : NV <= 16 ? 8 : 4;
+constexpr int kDeepBlock = 256;
+template <int NV, int MAXT, bool CBOW, bool HS, bool NS, bool REPLAY, bool WIDE>
+__global__ __launch_bounds__(kDeepBlock, 2) void train_epoch_deep_kernel(TrainArgs a) {
+  train_epoch<NV, MAXT, CBOW, HS, NS, REPLAY, WIDE>(a);
 }
 
 // Sequential target updates for w2v_dev_apply_rows (one wave): target t is

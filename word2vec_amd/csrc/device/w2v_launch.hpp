@@ -10,6 +10,7 @@ using ApplyFn = void (*)(float*, int64_t, int, const float*, float*, const uint8
 
 #define W2V_DECLARE_NV(N)                                            \
   KernelFn pick_train_nv##N(bool cbow, bool hs, bool ns, bool replay, bool wide); \
+  KernelFn pick_train_deep_nv##N(bool cbow); \
   ApplyFn pick_apply_nv##N();
 W2V_DECLARE_NV(1)
 W2V_DECLARE_NV(2)

@@ -242,9 +242,11 @@ class DeviceTrainer:
         self._chk(self.lib.w2v_dev_private_rate_used(self.h, C.byref(mu)), "w2v_dev_private_rate_used")
         wc = C.c_int64()
         self._chk(self.lib.w2v_dev_wave_cap_used(self.h, C.byref(wc)), "w2v_dev_wave_cap_used")
+        dp = C.c_int32()
+        self._chk(self.lib.w2v_dev_deep_used(self.h, C.byref(dp)), "w2v_dev_deep_used")
         return {"hot_rows": r.value, "hot_nodes": n.value, "private_rows": p.value, "context_rows": c.value,
                 "flush_centers": f.value, "context_flush": cf.value, "hot_tau_rows": tr.value,
-                "private_rate": round(mu.value, 4), "wave_cap": wc.value}
+                "private_rate": round(mu.value, 4), "wave_cap": wc.value, "deep": dp.value}
 
     def set_private_rows(self, n: int):
         """Hottest output rows privatised per workgroup in LDS: -1 auto (default), 0 off."""
