@@ -426,7 +426,7 @@ def test_configs3_own_size_eight_replicas(tmp_path):
 
 
 
-@pytest.mark.parametrize("R", [2, 8])
+@pytest.mark.parametrize("R", [8])  # R = 2 (the sum; +-0.02 in every round-5/6 suite) left for the time budget
 def test_shared_negatives_replicas_quality(R):
     """configs[4]'s shared-negatives minibatch (d512, negative 15) under a
     replica group (never run there): R same-device replicas, each
@@ -509,6 +509,9 @@ C3_SHAPE = dict(tokens=2_500_000_000, planted=0.05, planted_sents=0.02, seed=7)
 # delta at 64 / 96 / 128: -1.96 / -0.13 / -0.55 over two runs each,
 # profiles/r06f_replica_probe.log, r06g_replica_probe.log), so the similarity
 # low is north_star's -1 again (VERDICT r05 "next" 3).
+# The eight-replica side averages three runs (its similarity spreads ~1.6
+# points run to run, the single replica's ~0.9), so the -1 low is not a coin
+# toss on a -0.6 mean.
 C3_BOUNDS = {"analogy": (-1.0, 35.0), "similarity": (-1.0, 3.0)}
 
 
@@ -523,9 +526,9 @@ def test_configs3_shape_eight_replicas_hard_regime(tmp_path):
     vp = tmp_path / "vocab.txt"
     vp.write_text("".join(f"{i} {c} {t}\n" for i, (t, c) in enumerate(zip(data[2], data[1]))))
     ones = np.array([_class_on_ids(data, vp, None, seed=C3_SHAPE["seed"], dim=300) for _ in range(2)])
-    eights = np.array([_class_on_ids(data, vp, [0] * 8, seed=C3_SHAPE["seed"], dim=300) for _ in range(2)])
+    eights = np.array([_class_on_ids(data, vp, [0] * 8, seed=C3_SHAPE["seed"], dim=300) for _ in range(3)])
     d = eights.mean(0) - ones.mean(0)
-    print(f"configs[3] shape, eight replicas vs one (means of two): one {ones.round(2).tolist()} eight "
+    print(f"configs[3] shape, eight replicas vs one (means of three / two): one {ones.round(2).tolist()} eight "
           f"{eights.round(2).tolist()} delta {d.round(2)}")
     for k, metric in enumerate(("analogy", "similarity")):
         lo, hi = C3_BOUNDS[metric]
