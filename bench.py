@@ -163,7 +163,7 @@ def main():
     from word2vec_amd import _native as N
     from word2vec_amd import host
     from word2vec_amd.device import Config, DeviceTrainer
-    from word2vec_amd.replicas import (global_round_words, local_round_words, make_averager, n_rounds,
+    from word2vec_amd.replicas import (agree_rounds, global_round_words, local_round_words, make_averager, n_rounds,
                                        train_rounds)
 
     mode = MODES[args.mode]
@@ -274,8 +274,9 @@ def main():
     averager, rmode_used = make_averager(tr, mats, world, rank, rmode, not args.no_overlap, share)
     if args.sync_every > 0 or world == 1:
         rounds = n_rounds(n_sent * world, world, args.sync_every)
-    else:  # every rank's shard has ~ the same words: the same round count everywhere
+    else:  # every rank's shard has ~ the same words, but not exactly: agree on the largest round count
         rounds = max(1, -(-int(ids_h.size) // max(1, args.sync_words or config3_sync_words(world, rmode))))
+        rounds = agree_rounds(rounds, world)  # a rank that ran a different number of exchanges would hang the group
     order_dev = torch.arange(n_sent, dtype=torch.int64, device=dev)  # this rank's shard, in order
     round_words = global_round_words(local_round_words(soff_h, range(n_sent), rounds), world)
     progress = 0

@@ -11,7 +11,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from word2vec_amd.replicas import (TorchAverager, global_round_words, local_round_words, n_rounds, round_slices,
+from word2vec_amd.replicas import (TorchAverager, agree_rounds, global_round_words, local_round_words, n_rounds, round_slices,
                                    shard_range, train_rounds)
 
 
@@ -94,7 +94,9 @@ def _worker(rank, world, port, out):
         W.zero_()
         tr = FakeTrainer([W], rank)
         total = train_rounds(tr, TorchAverager([W], world), order, 0, R, 100, rw, world)
-        out.put((rank, tr.seen, total, W[0, 0].item(), tr.progress, rw))
+        # bench.py's per-rank round counts (a ceil of each rank's own shard) agree on the largest
+        agreed = agree_rounds(5 + rank, world)
+        out.put((rank, tr.seen, total, W[0, 0].item(), tr.progress, rw, agreed))
     finally:
         dist.destroy_process_group()
 
@@ -114,6 +116,7 @@ def test_gloo_replica_averaging_and_rounds(world):
     # every rank ran the same number of rounds; progress = 100 + 10 words x 15 sentences
     totals = {r[2] for r in res}
     assert totals == {100 + 10 * 15}
+    assert {r[6] for r in res} == {5 + world - 1}
     # the counter each rank starts a round from is the global count / world
     rw = res[0][5]
     assert sum(rw) == 150 and all(r[5] == rw for r in res)

@@ -60,6 +60,17 @@ def n_rounds(n_total: int, world: int, sync_every: int) -> int:
     return max(1, -(-largest // sync_every))
 
 
+def agree_rounds(rounds: int, world: int, group=None) -> int:
+    """The largest of the ranks' round counts (every rank must run the same
+    number of exchanges; shards of a synthetic or real corpus differ by a few
+    words, and a per-rank ceil near an integer would split them)."""
+    if world <= 1:
+        return rounds
+    t = torch.tensor([int(rounds)], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())
+
+
 def round_slices(n: int, rounds: int) -> list[tuple[int, int]]:
     """Cut [0, n) into `rounds` consecutive near-equal slices (some may be empty)."""
     return [(n * k // rounds, n * (k + 1) // rounds) for k in range(rounds)]
