@@ -395,8 +395,12 @@ def test_configs3_own_size_eight_replicas(tmp_path):
     from tests.planted_ids import planted_zipf_ids_torch, scores
     from word2vec_amd.model import Word2Vec
 
+    import time
+
+    t0 = time.time()
     dev = torch.device("cuda", 0)
     ids, counts, words, qs, prs, raw = planted_zipf_ids_torch(10_000_000_000, 1_000_000, 0.05, 11, dev)
+    t_gen = time.time() - t0
     assert raw == 10_000_000_000 and counts.size > 1_000_000
     vp = tmp_path / "vocab.txt"
     vp.write_text("".join(f"{i} {c} {t}\n" for i, (t, c) in enumerate(zip(words, counts))))
@@ -409,7 +413,9 @@ def test_configs3_own_size_eight_replicas(tmp_path):
     w.precalc_sampling()
     w.init_weights()
     n_sent, L = ids.shape
+    t1 = time.time()
     w.train_ids(ids.reshape(-1), np.arange(0, n_sent * L + 1, L, dtype=np.int64), raw)
+    t_train = time.time() - t1
     del ids
     secs = w.epoch_seconds
     assert w.current_words == raw  # no OOV: every token is an in-vocab word, counted once
@@ -421,7 +427,8 @@ def test_configs3_own_size_eight_replicas(tmp_path):
     a, sim = scores(words, E, qs, prs, dev)
     print(f"configs[3] own size (10 B tokens, V {counts.size}, d300, eight replicas on one GPU): "
           f"{raw / secs[0] / 1e6:.1f} M words/s, {w.replica_rounds} exchanges, replicas apart "
-          f"{w.replica_max_diff:.2e}, analogy {a:.2f} similarity {sim:.2f}")
+          f"{w.replica_max_diff:.2e}, analogy {a:.2f} similarity {sim:.2f}; seconds: corpus {t_gen:.1f}, train_ids "
+          f"{t_train:.1f} (epoch {secs[0]:.1f}), all {time.time() - t0:.1f}")
     assert a >= 95.0 and sim >= 70.0
 
 
@@ -515,18 +522,49 @@ C3_SHAPE = dict(tokens=2_500_000_000, planted=0.05, planted_sents=0.02, seed=7)
 C3_BOUNDS = {"analogy": (-1.0, 35.0), "similarity": (-1.0, 3.0)}
 
 
-def test_configs3_shape_eight_replicas_hard_regime(tmp_path):
+_C3_SHAPE_CACHE = {}
+
+
+def _c3_shape_data(tmp_dir):
+    """The hard-regime corpus and its vocab file, built once per session."""
     import torch
 
     from tests.planted_ids import planted_zipf_ids_torch
 
-    data = planted_zipf_ids_torch(C3_SHAPE["tokens"], 1_000_000, C3_SHAPE["planted"], C3_SHAPE["seed"],
-                                  torch.device("cuda", 0), planted_sents=C3_SHAPE["planted_sents"])
-    assert data[1].size > 1_000_000  # every filler rank in vocab (V 1 M + the planted grid)
-    vp = tmp_path / "vocab.txt"
-    vp.write_text("".join(f"{i} {c} {t}\n" for i, (t, c) in enumerate(zip(data[2], data[1]))))
-    ones = np.array([_class_on_ids(data, vp, None, seed=C3_SHAPE["seed"], dim=300) for _ in range(2)])
+    if "data" not in _C3_SHAPE_CACHE:
+        data = planted_zipf_ids_torch(C3_SHAPE["tokens"], 1_000_000, C3_SHAPE["planted"], C3_SHAPE["seed"],
+                                      torch.device("cuda", 0), planted_sents=C3_SHAPE["planted_sents"])
+        assert data[1].size > 1_000_000  # every filler rank in vocab (V 1 M + the planted grid)
+        vp = tmp_dir / "c3_shape_vocab.txt"
+        vp.write_text("".join(f"{i} {c} {t}\n" for i, (t, c) in enumerate(zip(data[2], data[1]))))
+        _C3_SHAPE_CACHE["data"], _C3_SHAPE_CACHE["vp"] = data, vp
+    return _C3_SHAPE_CACHE["data"], _C3_SHAPE_CACHE["vp"]
+
+
+def _c3_shape_ones(tmp_dir):
+    """The single replica's two runs (cached: the gate below needs them)."""
+    if "ones" not in _C3_SHAPE_CACHE:
+        data, vp = _c3_shape_data(tmp_dir)
+        _C3_SHAPE_CACHE["ones"] = np.array([_class_on_ids(data, vp, None, seed=C3_SHAPE["seed"], dim=300)
+                                            for _ in range(2)])
+    return _C3_SHAPE_CACHE["ones"]
+
+
+# The gate in two tests so that no single test runs past ~2 minutes (each
+# class run is ~40 s): the single replica's runs, then the eight replicas'
+# runs and the bounds.
+def test_configs3_shape_single_replica(tmp_path_factory):
+    ones = _c3_shape_ones(tmp_path_factory.mktemp("c3shape"))
+    print(f"configs[3] shape, one replica (two runs): {ones.round(2).tolist()}")
+    assert np.isfinite(ones).all() and (ones[:, 1] > 60.0).all()
+
+
+def test_configs3_shape_eight_replicas_hard_regime(tmp_path_factory):
+    tmp = tmp_path_factory.mktemp("c3shape8")
+    data, vp = _c3_shape_data(tmp)
+    ones = _c3_shape_ones(tmp)
     eights = np.array([_class_on_ids(data, vp, [0] * 8, seed=C3_SHAPE["seed"], dim=300) for _ in range(3)])
+    _C3_SHAPE_CACHE.clear()  # 10 GB of host ids
     d = eights.mean(0) - ones.mean(0)
     print(f"configs[3] shape, eight replicas vs one (means of three / two): one {ones.round(2).tolist()} eight "
           f"{eights.round(2).tolist()} delta {d.round(2)}")
