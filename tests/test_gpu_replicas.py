@@ -375,6 +375,27 @@ def _class_on_ids(data, vocab_path, gpu_devices, seed=3, dim=100):
     return scores(words, w.matrix(0), qs, prs, torch.device("cuda", 0))
 
 
+_C3_FULL = {}
+
+
+def _c3_full_corpus():
+    """configs[3]'s 10 B-token corpus (ids on the host, 40 GB), built once."""
+    import torch
+
+    from tests.planted_ids import planted_zipf_ids_torch
+
+    if "data" not in _C3_FULL:
+        _C3_FULL["data"] = planted_zipf_ids_torch(10_000_000_000, 1_000_000, 0.05, 11, torch.device("cuda", 0))
+    return _C3_FULL["data"]
+
+
+def test_configs3_own_size_corpus():
+    """The corpus of the test below, in a test of its own (~20 s) so that no
+    single test runs past ~2 minutes."""
+    ids, counts, words, qs, prs, raw = _c3_full_corpus()
+    assert raw == 10_000_000_000 and ids.size == raw and counts.size > 1_000_000 and int(counts.sum()) == raw
+
+
 def test_configs3_own_size_eight_replicas(tmp_path):
     """BASELINE configs[3] at its own size (VERDICT r05 "next" 4): a 10 B-token
     synthetic Zipf corpus over 1 M filler ranks (V 1,000,800 with the planted
@@ -392,14 +413,15 @@ def test_configs3_own_size_eight_replicas(tmp_path):
     shard alone learns them)."""
     import torch
 
-    from tests.planted_ids import planted_zipf_ids_torch, scores
+    from tests.planted_ids import scores
     from word2vec_amd.model import Word2Vec
 
     import time
 
     t0 = time.time()
     dev = torch.device("cuda", 0)
-    ids, counts, words, qs, prs, raw = planted_zipf_ids_torch(10_000_000_000, 1_000_000, 0.05, 11, dev)
+    ids, counts, words, qs, prs, raw = _c3_full_corpus()
+    _C3_FULL.clear()
     t_gen = time.time() - t0
     assert raw == 10_000_000_000 and counts.size > 1_000_000
     vp = tmp_path / "vocab.txt"
