@@ -94,10 +94,11 @@ def _paired_delta(name, mode, max_waves, seeds=None):
 
 @pytest.mark.parametrize("name,mode", [(n, m) for n in paired.ONE_WAVE_CORPORA for m in paired.PAIRED_MODES[n]])
 def test_quality_paired_one_wave_within_1(name, mode):
-    # two of the planted corpus's three seeds: one wavefront trains ~60 K words/s
-    # and the one-wave deltas sit within 0.06 of the oracle, so
-    # the third seed bought ~55 s of the suite's time budget and no resolution
-    d, got, ref = _paired_delta(name, mode, max_waves=1, seeds=2)
+    # one seed per corpus: one wavefront trains ~60 K words/s and the one-wave
+    # deltas sit within 0.06 of the oracle on every seed (round 6
+    # two seeds: -0.03..0.00, per seed identical to 0.01), so more seeds bought
+    # minutes of the suite's 900-s budget and no resolution
+    d, got, ref = _paired_delta(name, mode, max_waves=1, seeds=1)
     assert abs(d[0]) <= 1.0 and abs(d[1]) <= 1.0, (name, mode, got, ref)
 
 
