@@ -1556,12 +1556,32 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   a.ctx_M = nullptr;
   a.ctx_n = 0;
   a.ctx_flush_every = h->context_flush > 0 ? h->context_flush : (h->cfg.hs ? 32 : 256);
+  // Large-vocabulary HS (wide_hs_rule) under its wave cap: the top Huffman
+  // nodes in LDS as a write-combining cache, not a damped average — the
+  // workgroup's waves read node + pending delta (each wave's own updates stay
+  // visible to it, as the reference's thread sees its own), and the pending
+  // deltas are added to HBM as a plain SUM after every center of a wave
+  // (flush_every = waves per workgroup). Every node a wave's path visits is
+  // updated once per center in HBM instead of once per context: SG-HS at
+  // configs[2]'s scale -0.66 / +0.11 against the sequential golden at ~2x the
+  // speed (profiles/r06p_1_*; a flush every 8 centers -1.54 / -0.06). The
+  // cap's waves per CU decide the LDS budget (1 workgroup per CU for
+  // skip-gram's 256 waves: 127 nodes at d300). Skip-gram only: CBOW-HS's 1536
+  // waves share a cache four waves to a workgroup, and with it configs[2]'s
+  // corpus scored -0.16..-0.62 against the sequential golden in two runs
+  // (38.5 M words/s, 2x) and DIVERGED in the third (profiles/r06q_*, r06r_*).
+  const bool plain_cache = wide_hs_rule(h) && !h->cfg.cbow && h->private_rows < 0 && max_waves > 0 && !sn_fn;
   if (h->sched == W2V_SCHED_PARALLEL) {  // the reference-exact schedule keeps per-update rounding
     const int64_t row_bytes = (int64_t)h->nv * w2v::kWave * (int64_t)sizeof(float);
     int64_t per_wave = 10 * 1024;
     if (h->knobs.lds_per_wave > 0) per_wave = h->knobs.lds_per_wave;  // experiments
-    const int64_t budget =
+    int64_t budget =
         std::min<int64_t>(160 * 1024, per_wave * (int64_t)wpb) - 4 * w2v::lds_header_words(w2v::kPrivMax, 64);
+    if (plain_cache) {
+      const int64_t n_cu = h->n_cu > 0 ? h->n_cu : 1;
+      const int64_t wg_per_cu = std::max<int64_t>(1, ((max_waves + n_cu - 1) / n_cu + wpb - 1) / wpb);
+      budget = 160 * 1024 / wg_per_cu - 4 * w2v::lds_header_words(w2v::kPrivMax, 64);
+    }
     int64_t fit = budget / row_bytes;
     // <= 64 output rows by default for CBOW and HS. Skip-gram NS takes
     // kSgNsPrivRows (96), on a large vocabulary (>= kWidePrivVocab) up to 128,
@@ -1581,7 +1601,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
                               : !sg_ns ? (wide_hs ? kCbowHsPrivNodes : 64)
                                        : h->V >= kWidePrivVocab ? w2v::kPrivMax : kSgNsPrivRows;
     const bool plain_hs = wide_hs_rule(h);  // large-vocabulary HS: no LDS-private nodes / context rows
-    int64_t P = std::min<int64_t>(fit, h->private_rows > 0 ? w2v::kPrivMax : plain_hs ? 0 : auto_rows);
+    int64_t P = std::min<int64_t>(fit, h->private_rows > 0 || plain_cache ? w2v::kPrivMax : plain_hs ? 0 : auto_rows);
     if (h->private_rows >= 0) P = std::min<int64_t>(P, h->private_rows);
     const bool hs = h->cfg.hs != 0;
     const int64_t avail = hs ? h->V - 1 : h->V;
@@ -1597,6 +1617,10 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
       a.priv_M = hs ? h->S : (h->cfg.cbow ? h->W : h->C);
       a.priv_lo = (int32_t)(hs ? avail - P : 0);  // HS: the P internal nodes nearest the root (V-2)
       a.priv_n = (int32_t)P;
+      if (plain_cache) {  // a write-combining cache: summed, flushed after every center of a wave
+        a.priv_avg = 0.0f;
+        if (h->flush_centers <= 0) a.flush_every = wpb;
+      }
     }
     // Auto for CBOW. It doubles CBOW-HS throughput and raises its planted-
     // corpus scores. CBOW-NS (hot rows privatised on both sides of every dot
@@ -1729,7 +1753,10 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     const int threads = wpb * w2v::kWave;
     int per_cu = 0, per_cu_occ = 0;
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds_bytes));
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_occ, occ_fn, threads, lds_bytes));
+    // (the write-combining node cache of a capped HS launch does not change
+    // which nodes the chip's waves contend on: its hot set is counted as
+    // without the cache, the set its quality was measured with)
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_occ, occ_fn, threads, plain_cache ? 0 : lds_bytes));
     if (per_cu < 1) per_cu = 1;
     if (per_cu_occ < 1) per_cu_occ = 1;
     const int64_t resident = (int64_t)per_cu * h->n_cu;
@@ -1792,7 +1819,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   // helps small launches (CBOW-HS in 16 slices per epoch, text8-like: analogy
   // 24.5 vs 12.2) but over-damps a corpus with fewer sentences than the chip
   // holds waves (planted CBOW-HS: similarity -13 vs the oracle; profiles/r02l_*, r02r_*).
-  if (h->sched == W2V_SCHED_PARALLEL && h->cfg.hs && a.priv_n + a.ctx_n > 0) {
+  if (h->sched == W2V_SCHED_PARALLEL && h->cfg.hs && a.priv_n + a.ctx_n > 0 && !plain_cache) {
     const int32_t fe = auto_hs_flush(h, count, (int64_t)grid.x);
     if (h->flush_centers <= 0) a.flush_every = fe;
     if (h->context_flush <= 0) a.ctx_flush_every = std::max<int32_t>(1, fe / 2);
