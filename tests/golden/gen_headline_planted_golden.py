@@ -48,10 +48,15 @@ WORKLOADS = {
     "c2ns": dict(corpus=TEXT8, mode="cbow_ns", dim=200, negative=5, alpha=0.05),
     # the reference's SG-HS mode on configs[0]'s corpus and width
     "c1hs": dict(corpus=TEXT8, mode="sg_hs", dim=100, negative=0, alpha=0.025),
-    # SG-HS at configs[2]'s corpus and width (probe golden; no test reads it)
+    # SG-HS at configs[2]'s corpus and width
     "c3hs": dict(corpus=dict(n_tokens=50_000_000, filler=1_000_000, planted_frac=0.05), mode="sg_hs", dim=300,
                  negative=0, alpha=0.025),
-    # CBOW-HS at configs[2]'s corpus and width (probe golden; no test reads it)
+    # SG-HS between text8's and configs[2]'s vocabularies (round 6 probe golden,
+    # no gate: where does the large-vocabulary HS rule's threshold belong?
+    # DESIGN.md §4.1): 20 M tokens, Zipf(s=1) filler over 300 K ranks, d200
+    "mhs": dict(corpus=dict(n_tokens=20_000_000, filler=300_000, planted_frac=0.05), mode="sg_hs", dim=200,
+                negative=0, alpha=0.025),
+    # CBOW-HS at configs[2]'s corpus and width
     "c3cbhs": dict(corpus=dict(n_tokens=50_000_000, filler=1_000_000, planted_frac=0.05), mode="cbow_hs", dim=300,
                    negative=0, alpha=0.05),
 }
