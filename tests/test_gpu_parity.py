@@ -93,6 +93,40 @@ def test_philox_sequential_deep_hs(mode, dim, monkeypatch):
     d.close()
 
 
+def test_one_wave_large_vocab_hs_policy(monkeypatch):
+    """The large-vocabulary HS policy's parallel path — the wave cap, the deep
+    kernel and skip-gram's per-wave write-combining node cache (summed after
+    every center) — forced at a small vocabulary (W2V_WIDE_HS=1) and run on ONE
+    wave of the parallel Philox schedule, where it must train what the
+    sequential oracle does: each wave reads node + its own pending delta, so
+    the cache keeps the reference's per-thread view (sentences <= 128 tokens:
+    one work item per sentence, the alpha refresh at sentence starts as in the
+    sequential loop)."""
+    sents = zipf_sentences(60, 120, 400, seed=43, ragged=True)
+    o = oracle_run(sents, "sg_hs", dim=300, window=5, iters=1, table_size=100_000, train=False)
+    o.build_sample()
+    cfg = device_config(o, "sg_hs", 300, 5, 1, 100_000, True, 0.05, 2.5e-6)
+    monkeypatch.setenv("W2V_WIDE_HS", "1")
+    d = device_from_oracle(o, cfg, initial=False)
+    monkeypatch.delenv("W2V_WIDE_HS")
+    init = [o.matrix(k) for k in range(3)]
+    key = 0x0DEE_9000_0000_7777
+    order = np.random.default_rng(7).permutation(o.samples()[1].size - 1)
+    o.train_philox(0, 1, order, key, 0)
+    d.set_rng(N.W2V_RNG_PHILOX, key)
+    d.set_schedule(N.W2V_SCHED_PARALLEL)
+    d.set_max_waves(1)
+    d.set_progress(0)
+    st = d.train_epoch(0, order)
+    pol = d.policy()
+    assert pol["deep"] == 1 and pol["private_rows"] > 0 and pol["flush_centers"] == 1, pol
+    assert st["words"] == o.current_words
+    got = d.download_model()
+    want = [o.matrix(k) if got[k] is not None else None for k in range(3)]
+    check_parity(got, want, init, *MULTI, tag="one-wave large-vocabulary HS policy sg_hs d300")
+    d.close()
+
+
 @pytest.mark.parametrize("mode", list(MODES))
 @pytest.mark.parametrize("dim", [48, 100, 200, 300, 512])
 def test_replay_single_sentence(mode, dim):
