@@ -356,3 +356,34 @@ def test_quality_headline_scale(name):
         dev = DEVIATION_HIGH.get(name, {}).get(metric)
         top = refs[0][k] + dev if dev is not None else hi + 1.0
         assert got[k] <= top, (name, metric, "above the bound", got, refs, top)
+
+
+# configs[0]'s corpus under an explicit wave cap that keeps 16-wave workgroups
+# but halves their number (4096 waves): with the uncapped launch's 112 private
+# rows it collapsed to -69 analogy (a cap of 2048: -41); skip-gram NS keeps 64
+# rows on a capped launch (w2v_dev.hip tail_ok; profiles/r06aj_c1_probe.log,
+# r06ak_c1_probe.log). One golden seed, the same floor as the uncapped gate.
+def test_quality_headline_c1_wave_capped():
+    import torch
+
+    from tests.golden import gen_headline_planted_golden as G
+    from tests.planted_ids import gpu_trainer, scores
+
+    name = "c1"
+    gold = json.loads(G.golden_path(name).read_text())
+    w = G.WORKLOADS[name]
+    ids, soff, counts, words, raw, qs, prs = G.corpus(name)
+    r = gold["scores"][0]
+    W0, C0, S0, key = G.init(name, r["seed"], counts.size)
+    t = gpu_trainer(counts, ids, soff, raw, w["mode"], w["dim"], w["negative"], w["alpha"], W0, C0, S0, key,
+                    window=G.TRAIN["window"], subsample=G.TRAIN["subsample"], table_size=G.TRAIN["table_size"])
+    t.set_max_waves(4096)
+    st = t.train_epoch(0, G.order_of(r["seed"], soff.size - 1))
+    pol = t.policy()
+    W, _, _ = t.download_model()
+    t.close()
+    got = np.array(scores(words, W, qs, prs, torch.device("cuda", 0)))
+    ref = [r["analogy"], r["similarity"]]
+    print(f"headline-scale c1 at 4096 waves, seed {r['seed']}: gpu {got.round(2)} sequential {ref} policy {pol}")
+    assert st["nonfinite"] == 0 and pol["private_rows"] == 64
+    assert got[0] >= ref[0] - 1.0 and got[1] >= ref[1] - 1.0, (got, ref)

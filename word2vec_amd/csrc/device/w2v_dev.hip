@@ -1617,8 +1617,18 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     const bool sg_ns = !h->cfg.cbow && !h->cfg.hs;
     const bool wide_hs = h->cfg.cbow && h->cfg.hs && h->V >= kWideHsVocab && fit >= kCbowHsPrivNodes + w2v::kCtxMax - 1;
     const bool sg_hs = !h->cfg.cbow && h->cfg.hs;
+    // Skip-gram NS rows past the 64th only on an uncapped launch: they were
+    // measured (and their tail average set) with the chip's whole grid. Under a
+    // wave cap that leaves 16- or 8-wave workgroups but fewer of them, the
+    // top rows' flush scale (priv_scales: per launch workgroup) doubles, and
+    // together with the tail rows configs[0]'s corpus collapsed: 2048 / 4096
+    // waves -41.0 / -68.7 analogy against the sequential golden, 64 rows at the
+    // same caps -0.09 / +0.12, the uncapped launch at 112 rows -0.29
+    // (profiles/r06ai_c1_probe.log, r06aj_*, r06ak_*).
+    const bool tail_ok = max_waves <= 0;
     const int64_t auto_rows = sg_hs ? w2v::kPrivMax
                               : !sg_ns ? (wide_hs ? kCbowHsPrivNodes : 64)
+                              : !tail_ok ? 64
                                        : h->V >= kWidePrivVocab ? w2v::kPrivMax : kSgNsPrivRows;
     const bool plain_hs = wide_hs_rule(h);  // large-vocabulary HS: no LDS-private nodes / context rows
     int64_t P = std::min<int64_t>(fit, h->private_rows > 0 || plain_cache ? w2v::kPrivMax : plain_hs ? 0 : auto_rows);
