@@ -1778,7 +1778,7 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   KernelFn fn = deep ? kernel_deep_for(h) : occ_fn;
   HIP_TRY(hipMemsetAsync(h->work, 0, sizeof(unsigned int), h->stream));
   dim3 grid(1), block(64);
-  int64_t resident_waves = 1, resident_wg = 1;
+  int64_t resident_waves = 1, resident_wg = 1, uncapped_wg = 1;
   if (h->sched == W2V_SCHED_PARALLEL) {
     const int threads = wpb * w2v::kWave;
     int per_cu = 0, per_cu_occ = 0;
@@ -1792,6 +1792,8 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
     const int64_t resident = (int64_t)per_cu * h->n_cu;
     resident_waves = (int64_t)per_cu_occ * h->n_cu * (max_wpb);
     resident_wg = resident;
+    // the workgroups of max_wpb waves the launch would run without its cap
+    uncapped_wg = std::min<int64_t>((count + max_wpb - 1) / max_wpb, (int64_t)per_cu_occ * wpb * h->n_cu / max_wpb);
     const int64_t need = (count + wpb - 1) / wpb;
     int64_t g = need < resident ? need : resident;
     if (max_waves > 0 && (max_waves + wpb - 1) / wpb < g) g = (max_waves + wpb - 1) / wpb;
@@ -1849,14 +1851,25 @@ static int launch_train(w2v_dev* h, int32_t epoch, const int64_t* order_dev, int
   // helps small launches (CBOW-HS in 16 slices per epoch, text8-like: analogy
   // 24.5 vs 12.2) but over-damps a corpus with fewer sentences than the chip
   // holds waves (planted CBOW-HS: similarity -13 vs the oracle; profiles/r02l_*, r02r_*).
+  // A wave cap that keeps the uncapped launch's workgroup shape runs fewer of
+  // its workgroups; the flush interval and scales then count the uncapped
+  // launch's workgroups, the ones they were measured with. Counted from the
+  // capped grid, c1hs (SG-HS, configs[0]'s corpus) at 4096 waves collapsed to
+  // -43.9 analogy against the sequential golden (the uncapped launch +2.8),
+  // counted this way +17.7 (profiles/r06al_c1hs_probe.log, r06an_*). Narrower
+  // workgroups keep their own grid: at 2048 waves (8-wave workgroups) the
+  // uncapped count moved configs[1]'s corpus from -1.7 to -4.2, and one wave's
+  // flush must stay its own exact sum.
+  int64_t g_flush = (int64_t)grid.x;
+  if (max_waves > 0 && wpb == max_wpb && h->sched == W2V_SCHED_PARALLEL) g_flush = std::max(g_flush, uncapped_wg);
   if (h->sched == W2V_SCHED_PARALLEL && h->cfg.hs && a.priv_n + a.ctx_n > 0 && !plain_cache) {
-    const int32_t fe = auto_hs_flush(h, count, (int64_t)grid.x);
+    const int32_t fe = auto_hs_flush(h, count, g_flush);
     if (h->flush_centers <= 0) a.flush_every = fe;
     if (h->context_flush <= 0) a.ctx_flush_every = std::max<int32_t>(1, fe / 2);
   }
   h->last_flush = a.priv_n > 0 ? a.flush_every : 0;
   h->last_ctx_flush = a.ctx_n > 0 ? a.ctx_flush_every : 0;
-  priv_scales(h, a, h->knobs.scale_resident ? resident_wg : (int64_t)grid.x, false);
+  priv_scales(h, a, h->knobs.scale_resident ? resident_wg : g_flush, false);
   a.wide_ids = nullptr;
   a.wide_stride = 0;
   if (h->cfg.cbow && h->cfg.window > w2v::kMaxWideWindow) {  // cbow_center_huge: one id slice per wave
